@@ -1,0 +1,116 @@
+/*
+ * satmi.h -- C ABI of the MI355X-native clause-set solving path.
+ *
+ * The reference (andreistana05/SAT-MPI-Stana-Andrei) is one Python script,
+ * "comparatie intre algoritmii de rezolvare a seturilor de clauze.py" (REF.py).
+ * Its solver entry points are plain Python functions over `List[List[int]]`
+ * (REF.py:11-14); the drop-in mirror of those functions lives in
+ * sat-mpi-stana-andrei_amd/satmi/solvers.py and calls the entry points below
+ * through ctypes (INTEGRATION.md shows the binding).  All pointers are plain
+ * C pointers; "d_" pointers are HIP device pointers, "h_" pointers host memory.
+ * Every function returns SATMI_OK (0) or a negative error; satmi_last_error()
+ * describes the last failure of the calling thread.
+ *
+ * Formula layout (CSR, the "flat literal/offset arrays in HBM" of the design):
+ *   instance b owns clauses  [inst_clause_begin[b], inst_clause_begin[b+1])
+ *   clause   c owns literals [clause_lit_begin[c],  clause_lit_begin[c+1])
+ *   literals are DIMACS ints (v or -v, v >= 1), exactly the ints of REF.py's
+ *   Clause = List[int]; inst_nvars[b] = largest variable index of instance b.
+ */
+#ifndef SATMI_H
+#define SATMI_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SATMI_ABI_VERSION 1
+
+/* return codes */
+#define SATMI_OK 0
+#define SATMI_ERR_ARG (-1)
+#define SATMI_ERR_HIP (-2)
+#define SATMI_ERR_TOO_LARGE (-3)
+#define SATMI_ERR_NOMEM (-4)
+
+/* per-instance DPLL status (d_status[b]) */
+#define SATMI_DPLL_EXHAUSTED 0      /* search tree fully explored                 */
+#define SATMI_DPLL_STOPPED 1        /* stopped after max_solutions solutions      */
+#define SATMI_DPLL_NODE_LIMIT 2     /* node_limit calls reached                   */
+#define SATMI_DPLL_TIMEOUT 3        /* time_limit_s reached (REF.py:17, :417-437)  */
+#define SATMI_DPLL_TOO_LARGE 4      /* instance exceeds the launch's LDS layout   */
+
+/* DPLL modes */
+#define SATMI_MODE_REF 0    /* dpll_optimized exactly as REF.py:133-214             */
+#define SATMI_MODE_SOUND 1  /* same procedure, decisions applied as unit clauses   */
+
+/* counters per instance, d_counters[b*SATMI_NCOUNTERS + k] */
+#define SATMI_NCOUNTERS 8
+#define SATMI_CTR_NODES 0        /* dpll_optimized calls                         */
+#define SATMI_CTR_DECISIONS 1    /* branch assignments (REF.py:212)              */
+#define SATMI_CTR_UNIT_PROPS 2   /* unit-propagation assignments (REF.py:154)    */
+#define SATMI_CTR_PURE 3         /* pure-literal assignments (REF.py:189)        */
+#define SATMI_CTR_CONFLICTS 4    /* unit_propagate returned None (REF.py:168)    */
+#define SATMI_CTR_SOLUTIONS 5    /* solutions found (len of REF.py's result)     */
+#define SATMI_CTR_ROUNDS 6       /* unit-propagation rounds (clause scans)       */
+#define SATMI_CTR_RESERVED 7
+
+int satmi_abi_version(void);
+const char *satmi_last_error(void);
+int satmi_device_count(int *count);
+int satmi_set_device(int device);
+int satmi_synchronize(void);
+
+/* Device memory helpers, so a host program needs no other HIP binding. */
+int satmi_malloc(void **d_ptr, uint64_t bytes);
+int satmi_free(void *d_ptr);
+int satmi_memcpy_h2d(void *d_dst, const void *h_src, uint64_t bytes, void *stream);
+int satmi_memcpy_d2h(void *h_dst, const void *d_src, uint64_t bytes, void *stream);
+int satmi_stream_synchronize(void *stream);
+
+/*
+ * Batched DPLL: one wavefront per instance.  Replaces dpll_optimized
+ * (REF.py:133-214) for a batch of formulas.
+ *   mode           SATMI_MODE_REF | SATMI_MODE_SOUND
+ *   max_solutions  stop after this many solutions (0 = enumerate all, as REF.py)
+ *   node_limit     stop after this many dpll calls (0 = none)
+ *   time_limit_s   per-instance wall-clock limit (<= 0 = none)
+ *   max_vars/max_clauses/max_lits   maxima over the batch (size the LDS layout)
+ *   d_init_begin/d_init_lits        optional caller assignment (REF.py:133's
+ *                  `assignment`), as signed literals in dict order; may be NULL
+ *   sol_cap        solutions stored per instance; sol_stride >= max assignment size
+ *   outputs: d_status[B], d_counters[B*8], d_sol_len[B*sol_cap],
+ *            d_sol_lits[B*sol_cap*sol_stride] (signed literals in the
+ *            assignment dict's insertion order), d_root_len[B],
+ *            d_root_lits[B*sol_stride] (the caller's dict after the root's
+ *            unit_propagate, REF.py:167, which mutates it in place)
+ *   stream         hipStream_t (NULL = default stream); the call is asynchronous
+ */
+int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_clause_begin,
+                            const int32_t *d_clause_lit_begin, const int32_t *d_lits,
+                            const int32_t *d_inst_nvars, int max_vars, int max_clauses, int max_lits,
+                            const int32_t *d_init_begin, const int32_t *d_init_lits,
+                            int mode, int64_t max_solutions, int64_t node_limit, double time_limit_s,
+                            int sol_cap, int sol_stride,
+                            int32_t *d_status, int64_t *d_counters, int32_t *d_sol_len,
+                            int32_t *d_sol_lits, int32_t *d_root_len, int32_t *d_root_lits,
+                            void *stream);
+
+/* Same, from host arrays (allocates, copies, runs, copies back; synchronous). */
+int satmi_dpll_batch_host(int num_instances, const int32_t *h_inst_clause_begin,
+                          const int32_t *h_clause_lit_begin, const int32_t *h_lits,
+                          const int32_t *h_inst_nvars,
+                          const int32_t *h_init_begin, const int32_t *h_init_lits,
+                          int mode, int64_t max_solutions, int64_t node_limit, double time_limit_s,
+                          int sol_cap, int sol_stride,
+                          int32_t *h_status, int64_t *h_counters, int32_t *h_sol_len,
+                          int32_t *h_sol_lits, int32_t *h_root_len, int32_t *h_root_lits);
+
+/* LDS bytes one wavefront needs for an instance of this size (0 = unsupported). */
+uint64_t satmi_dpll_lds_bytes(int max_vars, int max_clauses, int max_lits);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

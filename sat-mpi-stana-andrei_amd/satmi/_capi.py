@@ -1,0 +1,93 @@
+"""ctypes binding of libsatmi.so (include/satmi.h).
+
+The library is built in-tree (`make -C sat-mpi-stana-andrei_amd`, or
+`__graft_entry__.build()`).  There is no CPU fallback: if the library or a GPU
+is missing, every solver call raises SatmiError.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsatmi.so")
+
+# include/satmi.h constants
+OK = 0
+MODE_REF = 0
+MODE_SOUND = 1
+NCOUNTERS = 8
+COUNTER_NAMES = ("nodes", "decisions", "unit_props", "pure_assigns", "conflicts", "solutions", "rounds",
+                 "reserved")
+DPLL_EXHAUSTED, DPLL_STOPPED, DPLL_NODE_LIMIT, DPLL_TIMEOUT, DPLL_TOO_LARGE = range(5)
+STATUS_NAMES = {0: "exhausted", 1: "stopped", 2: "node_limit", 3: "timeout", 4: "too_large"}
+RES_SAT, RES_UNSAT, RES_LIMIT = 1, 0, -1
+
+# exported symbols, checked by tests/test_capi_symbols.py against include/satmi.h
+EXPORTED = (
+    "satmi_abi_version", "satmi_last_error", "satmi_device_count", "satmi_set_device", "satmi_synchronize",
+    "satmi_malloc", "satmi_free", "satmi_memcpy_h2d", "satmi_memcpy_d2h", "satmi_stream_synchronize",
+    "satmi_dpll_batch_device", "satmi_dpll_batch_host", "satmi_dpll_lds_bytes",
+)
+
+
+class SatmiError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libsatmi.so (once).  torch is imported first when available so that
+    the process has exactly one HIP runtime (torch's libamdhip64.so.7 satisfies
+    the library's NEEDED entry)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  (shares its HIP runtime with libsatmi)
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise SatmiError(f"{LIB_PATH} is missing: build it with `make -C {os.path.dirname(_HERE)}` "
+                         "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    i32p, i64p, vp = P(ctypes.c_int32), P(ctypes.c_int64), ctypes.c_void_p
+    L.satmi_abi_version.restype = ctypes.c_int
+    L.satmi_last_error.restype = ctypes.c_char_p
+    L.satmi_device_count.argtypes = [P(ctypes.c_int)]
+    L.satmi_set_device.argtypes = [ctypes.c_int]
+    L.satmi_malloc.argtypes = [P(ctypes.c_void_p), ctypes.c_uint64]
+    L.satmi_free.argtypes = [vp]
+    L.satmi_memcpy_h2d.argtypes = [vp, vp, ctypes.c_uint64, vp]
+    L.satmi_memcpy_d2h.argtypes = [vp, vp, ctypes.c_uint64, vp]
+    L.satmi_stream_synchronize.argtypes = [vp]
+    L.satmi_dpll_lds_bytes.restype = ctypes.c_uint64
+    L.satmi_dpll_lds_bytes.argtypes = [ctypes.c_int] * 3
+    L.satmi_dpll_batch_device.argtypes = [
+        ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
+        ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+        vp, vp, vp, vp, vp, vp, vp]
+    L.satmi_dpll_batch_host.argtypes = [
+        ctypes.c_int, i32p, i32p, i32p, i32p, i32p, i32p,
+        ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+        i32p, i64p, i32p, i32p, i32p, i32p]
+    for name in EXPORTED:
+        getattr(L, name)  # AttributeError here = library/header mismatch
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != OK:
+        msg = load().satmi_last_error()
+        raise SatmiError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def require_gpu():
+    L = load()
+    n = ctypes.c_int(0)
+    rc = L.satmi_device_count(ctypes.byref(n))
+    if rc != OK or n.value < 1:
+        raise SatmiError("no HIP device visible: the satmi solvers run on MI355X only (no CPU fallback)")
+    return n.value
