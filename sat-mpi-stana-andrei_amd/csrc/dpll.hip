@@ -2,33 +2,39 @@
 //
 // Replaces dpll_optimized (REF.py:133-214) for batches of CNF formulas.
 //
-// Formulation (not the reference's list copying):
-//   * The instance (literals as 16-bit codes var<<1|neg, clause offsets) is
-//     staged once into the wave's LDS slice; the search never re-reads HBM.
-//   * The formula the reference keeps as filtered Python lists is represented
-//     implicitly by a per-variable state word vst[v]:
-//        bit0 assigned, bit1 value, bit2 "effective", bits3.. batch time + 1.
-//     A clause is in the reference's current formula iff none of its literals
-//     is true under an *effective* assignment; a literal is still in its clause
-//     iff it is not false under an effective assignment.  Unit propagation and
-//     pure-literal assignments are effective (they rewrite the formula in
-//     REF.py:156-164 / :190-194); in SATMI_MODE_REF a branch assignment is not
-//     (REF.py:210-213 never rewrites the formula) and in SATMI_MODE_SOUND it is.
-//   * unit_propagate (REF.py:139-165) processes a *snapshot* of unit clauses in
-//     clause order, one by one, and returns None at the first emptied clause.
-//     Here a round is: a wave-parallel clause scan that (a) finds the clauses
-//     emptied by the previous batch and the *time* (batch index) at which each
-//     was emptied -- the max time of its falsified literals -- and (b) collects
-//     the next snapshot of unit clauses in clause order with ballot/popcount
-//     compaction.  The batch itself is applied sequentially (it is short) so the
-//     first-come semantics of `if var in a` (REF.py:149-152) hold exactly.  The
-//     earliest emptied clause gives the exact stopping point, so assignment
-//     counts match the reference one for one.
-//   * Pure literals / branching (REF.py:174-208) use one clause-parallel scan
-//     with LDS atomics (count, first occurrence, sign set); pure literals are
-//     emitted in first-occurrence order through a position bitmap; the branch
-//     variable is a 64-bit wave max over (count, -first position), which is the
-//     reference's "first maximal key in dict order" tie-break.
+// Formulation (not the reference's list copying, and not a clause re-scan):
+//   * The instance is staged once into the wave's LDS slice: literal codes
+//     (var<<1 | negative, 16 bit), clause offsets, and per-literal occurrence
+//     lists (clause indices) built in LDS by a counting sort.  The search never
+//     touches HBM again until it writes the verdict.
+//   * The reference's shrinking formula (filtered Python lists) is represented
+//     by one 32-bit word per clause, cst[c] = nfree | ntrue << 16: nfree counts
+//     the literal occurrences not falsified by an *effective* assignment (the
+//     length of the reference's reduced clause), ntrue the occurrences made
+//     true (ntrue > 0 <=> the reference dropped the clause).  A clause is a
+//     unit clause of the reduced formula iff cst == 1 and is emptied iff
+//     nfree == 0.  Unit propagation and pure-literal assignments are effective
+//     (they rewrite the formula, REF.py:156-164 / :190-194); in
+//     SATMI_MODE_REF a branch assignment is not (REF.py:210-213 never rewrites
+//     the formula), in SATMI_MODE_SOUND it is.
+//   * Assigning literal l touches only the occurrence lists of l and -l, with
+//     LDS atomics on cst; the wave processes the flattened occurrences of a
+//     whole range of assignments at once (prefix sum over list lengths, owner
+//     lane found by a 6-step shuffle search).  Undo on backtrack is the exact
+//     inverse.  cnt[v] = positive | negative << 16 counts v's occurrences in
+//     active clauses and is maintained when a clause enters / leaves.
+//   * unit_propagate (REF.py:139-165) processes a *snapshot* of unit clauses
+//     in clause order.  A snapshot is assigned in parallel (first occurrence of
+//     a variable wins, exactly the `if var in a` rule of REF.py:149-152) with a
+//     time stamp = its index in the snapshot; a clause emptied by the batch was
+//     emptied at the max time stamp of its literals, so the reference's
+//     stopping point is the minimum of those, and the assignments after it are
+//     undone -- counts match the reference one for one.  Clauses that became
+//     unit are flagged in a bitmap; the next snapshot is the flagged clauses
+//     still unit, in clause order (ballot/popcount compaction).
+//   * Pure literals / branching (REF.py:174-208) read cnt per variable; first
+//     occurrences (the dict order of literal_sign / var_counts) are recovered
+//     from the occurrence lists only for the pure and the maximal variables.
 //   * Recursion is an explicit frame stack + trail in LDS.
 #include <hip/hip_runtime.h>
 
@@ -46,9 +52,11 @@ namespace satmi {
 constexpr uint32_t VS_ASSIGNED = 1u, VS_VALUE = 2u, VS_EFF = 4u, VS_FLAGS = 7u;
 constexpr int VS_TIME_SHIFT = 3;
 constexpr uint32_t PHASE_BIT = 0x8000u;
+constexpr uint32_t CST_TRUE1 = 0x10000u;   // one true literal occurrence in cst
+constexpr uint32_t NO_CLAIM = 0xFFFFFFFFu;
 
 struct DpllLayout {
-    uint32_t lit, coff, vst, trail, fvar, ftrail, units, cnt, first, sgn, posbits, bytes;
+    uint32_t lit, coff, occoff, occ, cst, vst, cnt, claim, trail, fvar, ftrail, units, ubits, posbits, bytes;
     int32_t lcap, mcap, ncap;
 };
 
@@ -77,206 +85,313 @@ struct DpllArgs {
 };
 
 struct Lds {
-    uint16_t *lit;      // [lcap]   literal codes
-    uint16_t *coff;     // [mcap+1] clause offsets into lit
-    uint32_t *vst;      // [ncap+1] variable state
-    uint16_t *trail;    // [ncap+1] assignment order (literal codes) == dict insertion order
-    uint16_t *fvar;     // [ncap+1] decision frames: var | PHASE_BIT once the False branch runs
-    uint16_t *ftrail;   // [ncap+1] trail length before the decision
-    uint16_t *units;    // [mcap+1] current unit-clause snapshot (literal codes)
-    uint32_t *cnt;      // [ncap+1] occurrence counts   (analyze scan)
-    uint32_t *first;    // [ncap+1] first occurrence    (analyze scan)
-    uint32_t *sgn;      // [ncap+1] sign set bit0 +, bit1 -
-    uint64_t *posbits;  // [lcap/64] pure literals by first position
+    uint16_t *lit;      // [lcap]      literal codes, clause-major (REF.py's clause lists)
+    uint16_t *coff;     // [mcap+1]    clause offsets into lit
+    uint16_t *occoff;   // [2ncap+3]   occurrence-list offsets per literal code
+    uint16_t *occ;      // [lcap]      clause index of every occurrence, grouped by literal code
+    uint32_t *cst;      // [mcap]      nfree | ntrue << 16
+    uint32_t *vst;      // [ncap+1]    assigned / value / effective bits, batch time + 1 above bit 3
+    uint32_t *cnt;      // [ncap+1]    occurrences in active clauses: positive | negative << 16
+    uint32_t *claim;    // [ncap+1]    first snapshot index claiming the variable (scratch)
+    uint16_t *trail;    // [ncap+1]    assignment order (literal codes) == dict insertion order
+    uint16_t *fvar;     // [ncap+1]    decision frames: var | PHASE_BIT once the False branch runs
+    uint16_t *ftrail;   // [ncap+1]    trail length before the decision
+    uint16_t *units;    // [mcap+1]    current unit-clause snapshot (literal codes)
+    uint64_t *ubits;    // [mcap/64]   clauses that became unit in the current batch
+    uint64_t *posbits;  // [lcap/64]   pure literals by first position
 };
 
-struct ScanRes {
-    int nu;      // units collected for the next batch
-    int e_min;   // earliest batch time at which a clause was emptied (INT_MAX: none)
-};
-
-// One unit-propagation scan over all clauses (see header).
-__device__ ScanRes scan_round(const Lds &S, int m) {
-    const int ln = lane_id();
-    const uint64_t lt = lanemask_lt();
-    int nu = 0;
-    int e_loc = INT_MAX;
-    for (int c0 = 0; c0 < m; c0 += 64) {
-        const int c = c0 + ln;
-        bool unit = false;
-        uint32_t ucode = 0;
-        if (c < m) {
-            const int beg = S.coff[c], end = S.coff[c + 1];
-            bool sat = false;
-            int alive = 0, emax = -1;
-            for (int j = beg; j < end; ++j) {
-                const uint32_t code = S.lit[j];
-                const uint32_t s = S.vst[code >> 1];
-                if (s & VS_EFF) {
-                    if (((s >> 1) ^ code) & 1u) {
-                        sat = true;   // satisfied (before or during the batch): never empty, never unit
-                    } else {
-                        emax = max(emax, (int)(s >> VS_TIME_SHIFT) - 1);
-                    }
-                } else {
-                    ++alive;
-                    ucode = code;
-                }
-            }
-            if (!sat) {
-                if (alive == 0) {
-                    if (emax >= 0) e_loc = min(e_loc, emax);
-                } else if (alive == 1) {
-                    unit = true;
-                }
-            }
-        }
-        const uint64_t mk = __ballot(unit);
-        if (unit) S.units[nu + __popcll(mk & lt)] = (uint16_t)ucode;
-        nu += __popcll(mk);
-    }
-    wave_sync();
-    return {nu, wave_min_i32(e_loc)};
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return uniform_u32(x);
 }
 
-// unit_propagate (REF.py:139-165).  Returns true on conflict.  `trail_len` is
-// advanced by every assignment made; `*exact_len` receives the trail length at
-// the exact point the reference stops (used for the root record).
-__device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, int nu, bool do_scan,
-                          bool decision_round, int64_t &props, int64_t &rounds, int *exact_len) {
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return uniform_u32(x);
+}
+
+// Apply (UNDO=false) or revert (UNDO=true) the effective assignments trail[beg, end):
+// clauses containing the literal gain/lose a true occurrence, clauses containing
+// its negation lose/regain a free occurrence.  All occurrences of the range are
+// processed by the wave at once.  Returns the change in the number of satisfied
+// clauses; for an apply, *e_min receives the earliest batch time at which a
+// clause was emptied (INT_MAX: none) and newly-unit clauses are flagged in ubits.
+template <bool UNDO>
+__device__ int apply_range(const Lds &S, int beg, int end, int *e_min) {
     const int ln = lane_id();
-    if (do_scan) {
-        ScanRes r = scan_round(S, m);
-        ++rounds;
-        nu = r.nu;
+    int dsat = 0;
+    int e_loc = INT_MAX;
+    for (int e0 = beg; e0 < end; e0 += 64) {
+        const int e = e0 + ln;
+        int b0 = 0, n0 = 0, b1 = 0, len = 0;
+        if (e < end) {
+            const uint32_t code = S.trail[e];
+            if (!UNDO || (S.vst[code >> 1] & VS_EFF)) {
+                b0 = S.occoff[code];
+                n0 = S.occoff[code + 1] - b0;
+                b1 = S.occoff[code ^ 1u];
+                len = n0 + (S.occoff[(code ^ 1u) + 1] - b1);
+            }
+        }
+        const int incl = wave_incl_scan(len);
+        const int start = incl - len;
+        const int total = __shfl(incl, 63, 64);
+        for (int f0 = 0; f0 < total; f0 += 64) {
+            const int f = f0 + ln;
+            // owner = last lane whose range starts at or before f
+            int o = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1) {
+                const int s = __shfl(start, o + step, 64);
+                if (s <= f) o += step;
+            }
+            const int r = f - __shfl(start, o, 64);
+            const int on0 = __shfl(n0, o, 64);
+            const int ob0 = __shfl(b0, o, 64);
+            const int ob1 = __shfl(b1, o, 64);
+            bool trans = false;
+            if (f < total) {
+                if (r < on0) {
+                    const uint32_t c = S.occ[ob0 + r];
+                    const uint32_t old = UNDO ? atomicSub(&S.cst[c], CST_TRUE1) : atomicAdd(&S.cst[c], CST_TRUE1);
+                    trans = (old >> 16) == (UNDO ? 1u : 0u);
+                    if (trans) {   // the clause leaves (re-enters) the reduced formula
+                        const int je = S.coff[c + 1];
+                        for (int j = S.coff[c]; j < je; ++j) {
+                            const uint32_t x = S.lit[j];
+                            const uint32_t inc = (x & 1u) ? 0x10000u : 1u;
+                            if (UNDO) atomicAdd(&S.cnt[x >> 1], inc);
+                            else atomicSub(&S.cnt[x >> 1], inc);
+                        }
+                    }
+                } else {
+                    const uint32_t c = S.occ[ob1 + (r - on0)];
+                    if (UNDO) {
+                        atomicAdd(&S.cst[c], 1u);
+                    } else {
+                        const uint32_t old = atomicSub(&S.cst[c], 1u);
+                        const uint32_t nf = (old & 0xFFFFu) - 1u;
+                        if (nf == 0u) {
+                            // emptied: at the latest time stamp among its (all false) literals
+                            int t = -1;
+                            const int je = S.coff[c + 1];
+                            for (int j = S.coff[c]; j < je; ++j)
+                                t = max(t, (int)(S.vst[S.lit[j] >> 1] >> VS_TIME_SHIFT) - 1);
+                            e_loc = min(e_loc, t);
+                        } else if (nf == 1u && (old >> 16) == 0u) {
+                            atomicOr((unsigned long long *)&S.ubits[c >> 6], 1ull << (c & 63));
+                        }
+                    }
+                }
+            }
+            dsat += __popcll(__ballot(trans));
+        }
     }
+    wave_sync();
+    if (!UNDO) *e_min = wave_min_i32(e_loc);
+    return UNDO ? -dsat : dsat;
+}
+
+__device__ void clear_ubits(const Lds &S, int m) {
+    for (int w = lane_id(); w < ((m + 63) >> 6); w += 64) S.ubits[w] = 0ull;
+    wave_sync();
+}
+
+// The next snapshot: clauses flagged in ubits that are still unit, in clause
+// order (REF.py:143), each represented by its one free literal.
+__device__ int collect_units(const Lds &S, int m) {
+    const int ln = lane_id();
+    const int W = (m + 63) >> 6;
+    int nu = 0;
+    for (int w0 = 0; w0 < W; w0 += 64) {
+        const int w = w0 + ln;
+        uint64_t bits = 0;
+        if (w < W) {
+            bits = S.ubits[w];
+            S.ubits[w] = 0ull;
+        }
+        uint64_t keep = 0;
+        for (uint64_t b = bits; b; b &= b - 1) {
+            const int c = w * 64 + (__ffsll((unsigned long long)b) - 1);
+            if (S.cst[c] == 1u) keep |= b & (~b + 1);   // ntrue == 0 and nfree == 1
+        }
+        const int kc = __popcll(keep);
+        const int incl = wave_incl_scan(kc);
+        int pos = nu + incl - kc;
+        for (; keep; keep &= keep - 1) {
+            const int c = w * 64 + (__ffsll((unsigned long long)keep) - 1);
+            uint32_t code = 0;
+            const int je = S.coff[c + 1];
+            for (int j = S.coff[c]; j < je; ++j) {
+                const uint32_t x = S.lit[j];
+                if (!(S.vst[x >> 1] & VS_EFF)) {
+                    code = x;
+                    break;
+                }
+            }
+            S.units[pos++] = (uint16_t)code;
+        }
+        nu += __shfl(incl, 63, 64);
+    }
+    wave_sync();
+    return uniform_i32(nu);
+}
+
+// unit_propagate (REF.py:139-165) from the snapshot S.units[0, nu).  Returns
+// true on conflict.  `trail_len` ends at the exact point the reference stops
+// (the assignments it made, including the one that emptied a clause).
+__device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, int nu, bool decision_round,
+                          int64_t &props, int64_t &rounds, int &nsat) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
     bool dec = decision_round;
-    // Every round that does not stop assigns at least one new variable, so at
-    // most nvars+1 rounds run; `guard` makes that bound structural.
+    // every batch that does not stop assigns >= 1 new variable: at most nvars+1 batches
     for (int guard = 0; nu > 0 && guard <= 32768; ++guard) {
+        ++rounds;
         const int round_start = trail_len;
-        bool mismatch = false;
-        int nassign = 0, first_k = -1;
-        for (int k = 0; k < nu; ++k) {
-            const uint32_t code = uniform_u32(S.units[k]);
-            const uint32_t v = code >> 1;
-            const uint32_t want = (code & 1u) ? 0u : VS_VALUE;
-            const uint32_t s = uniform_u32(S.vst[v]);
-            if (s & VS_ASSIGNED) {
-                if ((s & VS_VALUE) != want) { mismatch = true; break; }
-                continue;
+        // (1) variables assigned before this snapshot: equal value -> `continue`,
+        //     different value -> conflict at that unit (REF.py:149-151)
+        int kmis = INT_MAX;
+        for (int k0 = 0; k0 < nu; k0 += 64) {
+            const int k = k0 + ln;
+            if (k < nu) {
+                const uint32_t code = S.units[k];
+                const uint32_t s = S.vst[code >> 1];
+                if (s & VS_ASSIGNED) {
+                    if (((s >> 1) & 1u) == (code & 1u)) kmis = min(kmis, k);
+                } else {
+                    atomicMin(&S.claim[code >> 1], (uint32_t)k);
+                }
             }
-            if (ln == 0) {
-                S.vst[v] = VS_ASSIGNED | VS_EFF | want | ((uint32_t)(k + 1) << VS_TIME_SHIFT);
-                S.trail[trail_len] = (uint16_t)code;
+        }
+        kmis = wave_min_i32(kmis);
+        wave_sync();
+        // (2) the first occurrence of each variable before the mismatch is assigned,
+        //     in snapshot order, time-stamped with its snapshot index (REF.py:154)
+        const int lim = min(nu, kmis);
+        int nassign = 0, first_k = INT_MAX;
+        for (int k0 = 0; k0 < lim; k0 += 64) {
+            const int k = k0 + ln;
+            bool first = false;
+            uint32_t code = 0;
+            if (k < lim) {
+                code = S.units[k];
+                first = S.claim[code >> 1] == (uint32_t)k;
             }
-            if (first_k < 0) first_k = k;
-            ++trail_len;
-            ++nassign;
-            wave_sync();
+            const uint64_t mk = __ballot(first);
+            if (first) {
+                S.trail[trail_len + nassign + __popcll(mk & lt)] = (uint16_t)code;
+                S.vst[code >> 1] = VS_ASSIGNED | VS_EFF | ((code & 1u) ? 0u : VS_VALUE) |
+                                   ((uint32_t)(k + 1) << VS_TIME_SHIFT);
+            }
+            if (mk && first_k == INT_MAX) first_k = k0 + __ffsll((unsigned long long)mk) - 1;
+            nassign += __popcll(mk);
         }
         wave_sync();
-        if (nassign == 0 && !mismatch) break;   // `changed` stayed False (REF.py:141-142)
-        ScanRes r = scan_round(S, m);
-        ++rounds;
-        int e_min = r.e_min;
-        if (has_empty && nassign > 0) e_min = min(e_min, first_k);
+        for (int k = ln; k < nu; k += 64) S.claim[S.units[k] >> 1] = NO_CLAIM;
+        trail_len += nassign;
+        wave_sync();
+        // (3) reduce the formula by the batch (REF.py:156-164)
+        int e_min = INT_MAX;
+        nsat += apply_range<false>(S, round_start, trail_len, &e_min);
+        if (has_empty && nassign > 0) e_min = min(e_min, first_k);   // `[]` empties at the first reduction
         if (e_min != INT_MAX) {
-            int cnt = 0;
+            // the reference stopped at the unit with time stamp e_min: undo the rest
+            int keep = 0;
             for (int i0 = round_start; i0 < trail_len; i0 += 64) {
                 const int i = i0 + ln;
                 bool p = false;
-                if (i < trail_len) {
-                    const uint32_t s = S.vst[S.trail[i] >> 1];
-                    p = (int)(s >> VS_TIME_SHIFT) - 1 <= e_min;
-                }
-                cnt += __popcll(__ballot(p));
+                if (i < trail_len) p = (int)(S.vst[S.trail[i] >> 1] >> VS_TIME_SHIFT) - 1 <= e_min;
+                keep += __popcll(__ballot(p));
             }
-            props += cnt - (dec ? 1 : 0);
-            *exact_len = round_start + cnt;
+            const int cut = round_start + keep;
+            nsat += apply_range<true>(S, cut, trail_len, nullptr);
+            for (int i = round_start + ln; i < trail_len; i += 64) {
+                const uint32_t v = S.trail[i] >> 1;
+                S.vst[v] = i < cut ? (S.vst[v] & VS_FLAGS) : 0u;
+            }
+            trail_len = cut;
+            props += keep - (dec ? 1 : 0);
+            clear_ubits(S, m);
             return true;
         }
-        props += nassign - (dec ? 1 : 0);
-        for (int i = round_start + ln; i < trail_len; i += 64) {
-            const uint32_t v = S.trail[i] >> 1;
-            S.vst[v] &= VS_FLAGS;
-        }
-        wave_sync();
-        if (mismatch) {
-            *exact_len = trail_len;
-            return true;
-        }
+        props += nassign - (dec && nassign > 0 ? 1 : 0);
         dec = false;
-        nu = r.nu;
+        for (int i = round_start + ln; i < trail_len; i += 64) S.vst[S.trail[i] >> 1] &= VS_FLAGS;
+        wave_sync();
+        if (kmis != INT_MAX) {
+            clear_ubits(S, m);
+            return true;
+        }
+        if (nassign == 0) break;   // `changed` stayed False (REF.py:141-142)
+        nu = collect_units(S, m);
     }
-    *exact_len = trail_len;
     return false;
 }
 
+// First occurrence of variable v in the reduced formula (position in lit), the
+// key of literal_sign / var_counts' dict order (REF.py:174-179, :198-203).
+// Requires v to occur in an active clause.
+__device__ uint32_t first_position(const Lds &S, uint32_t v) {
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t code = v << 1; code <= ((v << 1) | 1u); ++code) {
+        const int e = S.occoff[code + 1];
+        for (int i = S.occoff[code]; i < e; ++i) {
+            const uint32_t c = S.occ[i];
+            if (c < best && (S.cst[c] >> 16) == 0u) best = c;
+        }
+    }
+    if (best == 0xFFFFFFFFu) return 0xFFFFFFFFu;
+    const int je = S.coff[best + 1];
+    for (int j = S.coff[best]; j < je; ++j)
+        if ((uint32_t)(S.lit[j] >> 1) == v) return (uint32_t)j;
+    return 0xFFFFFFFFu;
+}
+
 struct AnRes {
-    int nactive;
     int npure;
     uint32_t best_var;   // 0 = no unassigned variable occurs (REF.py:205)
 };
 
-// literal_sign / pure_literals / var_counts (REF.py:174-208) in one scan.
-__device__ AnRes analyze(const Lds &S, int m, int n) {
+// literal_sign / pure_literals / var_counts (REF.py:174-208).
+__device__ AnRes analyze(const Lds &S, int n) {
     const int ln = lane_id();
-    for (int v = ln; v <= n; v += 64) {
-        S.cnt[v] = 0;
-        S.first[v] = 0xFFFFFFFFu;
-        S.sgn[v] = 0;
-    }
-    wave_sync();
-    int nactive = 0;
-    for (int c0 = 0; c0 < m; c0 += 64) {
-        const int c = c0 + ln;
-        bool active = false;
-        if (c < m) {
-            const int beg = S.coff[c], end = S.coff[c + 1];
-            active = true;
-            for (int j = beg; j < end; ++j) {
-                const uint32_t code = S.lit[j];
-                const uint32_t s = S.vst[code >> 1];
-                if ((s & VS_EFF) && (((s >> 1) ^ code) & 1u)) { active = false; break; }
-            }
-            if (active) {
-                for (int j = beg; j < end; ++j) {
-                    const uint32_t code = S.lit[j];
-                    const uint32_t v = code >> 1;
-                    if (!(S.vst[v] & VS_ASSIGNED)) {
-                        atomicAdd(&S.cnt[v], 1u);
-                        atomicMin(&S.first[v], (uint32_t)j);
-                        atomicOr(&S.sgn[v], 1u << (code & 1u));
-                    }
-                }
-            }
-        }
-        nactive += __popcll(__ballot(active));
-    }
-    wave_sync();
     int npure = 0;
-    uint64_t best = 0;
+    uint32_t maxc = 0;
     for (int v0 = 1; v0 <= n; v0 += 64) {
         const int v = v0 + ln;
         bool pure = false;
-        if (v <= n) {
+        if (v <= n && !(S.vst[v] & VS_ASSIGNED)) {
             const uint32_t c = S.cnt[v];
-            if (c > 0) {
-                const uint32_t f = S.first[v];
-                pure = S.sgn[v] != 3u;
-                if (pure) atomicOr((unsigned long long *)&S.posbits[f >> 6], 1ull << (f & 63));
-                const uint64_t key = ((uint64_t)c << 32) | (uint64_t)(0xFFFFFFFFu - f);
-                best = key > best ? key : best;
+            const uint32_t p = c & 0xFFFFu, q = c >> 16;
+            if (p + q) {
+                maxc = max(maxc, p + q);
+                if (p == 0u || q == 0u) {
+                    pure = true;
+                    const uint32_t f = first_position(S, (uint32_t)v);
+                    atomicOr((unsigned long long *)&S.posbits[f >> 6], 1ull << (f & 63));
+                }
             }
         }
         npure += __popcll(__ballot(pure));
     }
-    best = wave_max_u64(best);
+    maxc = wave_max_u32(maxc);
     wave_sync();
-    uint32_t best_var = 0;
-    if (best) best_var = uniform_u32(S.lit[0xFFFFFFFFu - (uint32_t)best] >> 1);
-    return {nactive, npure, best_var};
+    if (npure > 0 || maxc == 0) return {npure, 0u};
+    // max(var_counts.items(), key=count): the first maximal key in dict order
+    uint32_t bestf = 0xFFFFFFFFu;
+    for (int v0 = 1; v0 <= n; v0 += 64) {
+        const int v = v0 + ln;
+        if (v <= n && !(S.vst[v] & VS_ASSIGNED)) {
+            const uint32_t c = S.cnt[v];
+            if ((c & 0xFFFFu) + (c >> 16) == maxc) bestf = min(bestf, first_position(S, (uint32_t)v));
+        }
+    }
+    bestf = wave_min_u32(bestf);
+    return {0, uniform_u32(S.lit[bestf] >> 1)};
 }
 
 // Append the pure literals to the trail in first-occurrence order (REF.py:187-189).
@@ -295,7 +410,7 @@ __device__ int assign_pures(const Lds &S, int L, int trail_len) {
             bits &= bits - 1;
             const uint32_t p = (uint32_t)(w * 64 + bit);
             const uint32_t v = S.lit[p] >> 1;
-            const bool positive = S.sgn[v] == 1u;
+            const bool positive = (S.cnt[v] & 0xFFFFu) != 0u;
             S.trail[pos++] = (uint16_t)((v << 1) | (positive ? 0u : 1u));
             S.vst[v] = VS_ASSIGNED | VS_EFF | (positive ? VS_VALUE : 0u);
         }
@@ -314,17 +429,28 @@ __device__ void store_assignment(const Lds &S, int trail_len, int32_t *out) {
     }
 }
 
-enum { ST_PROP_SCAN = 0, ST_PROP_PENDING = 1, ST_ANALYZE = 2, ST_BACKTRACK = 3, ST_DONE = 4 };
+// Pop trail[ft, trail_len): revert the effective ones, clear every variable.
+__device__ void unassign_to(const Lds &S, int ft, int trail_len, int &nsat) {
+    nsat += apply_range<true>(S, ft, trail_len, nullptr);
+    for (int i = ft + lane_id(); i < trail_len; i += 64) S.vst[S.trail[i] >> 1] = 0u;
+    wave_sync();
+}
+
+enum { ST_PROPAGATE = 0, ST_ANALYZE = 1, ST_BACKTRACK = 2, ST_DONE = 3 };
 
 __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
     const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
     const int cb = A.inst_clause_begin[b], ce = A.inst_clause_begin[b + 1];
     const int m = ce - cb;
     const int lb = A.clause_lit_begin[cb], le = A.clause_lit_begin[ce];
     const int L = le - lb;
-    const int n = A.inst_nvars[b];
     const int ib = A.init_begin ? A.init_begin[b] : 0;
     const int nin = A.init_begin ? A.init_begin[b + 1] - ib : 0;
+    // variables of the caller's dict may lie beyond the formula's (REF.py:133)
+    int nmax = A.inst_nvars[b];
+    for (int i = ln; i < nin; i += 64) nmax = max(nmax, abs(A.init_lits[ib + i]));
+    const int n = -wave_min_i32(-nmax);
     int64_t *ctr = A.counters + (int64_t)b * SATMI_NCOUNTERS;
     if (m > A.lay.mcap || L > A.lay.lcap || n > A.lay.ncap || n < 0) {
         if (ln < SATMI_NCOUNTERS) ctr[ln] = 0;
@@ -341,9 +467,56 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
         S.lit[i] = (uint16_t)((v << 1) | (x < 0 ? 1u : 0u));
     }
     for (int i = ln; i <= m; i += 64) S.coff[i] = (uint16_t)(A.clause_lit_begin[cb + i] - lb);
-    for (int v = ln; v <= n; v += 64) S.vst[v] = 0;
+    for (int v = ln; v <= n; v += 64) {
+        S.vst[v] = 0u;
+        S.cnt[v] = 0u;
+        S.claim[v] = 0u;
+    }
+    for (int w = ln; w < ((m + 63) >> 6); w += 64) S.ubits[w] = 0ull;
     for (int w = ln; w < ((L + 63) >> 6); w += 64) S.posbits[w] = 0ull;
     wave_sync();
+    for (int c = ln; c < m; c += 64) S.cst[c] = (uint32_t)(S.coff[c + 1] - S.coff[c]);
+    for (int i = ln; i < L; i += 64) {
+        const uint32_t x = S.lit[i];
+        atomicAdd(&S.cnt[x >> 1], (x & 1u) ? 0x10000u : 1u);   // all clauses are active
+    }
+    wave_sync();
+    // occurrence-list offsets: exclusive scan over literal codes 0 .. 2n+1
+    {
+        int base = 0;
+        for (int v0 = 0; v0 <= n; v0 += 64) {
+            const int v = v0 + ln;
+            uint32_t p = 0, q = 0;
+            if (v <= n) {
+                const uint32_t c = S.cnt[v];
+                p = c & 0xFFFFu;
+                q = c >> 16;
+            }
+            const int tot = (int)(p + q);
+            const int incl = wave_incl_scan(tot);
+            if (v <= n) {
+                const int o = base + incl - tot;
+                S.occoff[2 * v] = (uint16_t)o;
+                S.occoff[2 * v + 1] = (uint16_t)(o + (int)p);
+            }
+            base += __shfl(incl, 63, 64);
+        }
+        if (ln == 0) S.occoff[2 * n + 2] = (uint16_t)L;
+    }
+    wave_sync();
+    for (int c = ln; c < m; c += 64) {
+        const int je = S.coff[c + 1];
+        for (int j = S.coff[c]; j < je; ++j) {
+            const uint32_t x = S.lit[j];
+            const uint32_t old = atomicAdd(&S.claim[x >> 1], (x & 1u) ? 0x10000u : 1u);
+            const uint32_t idx = (x & 1u) ? (old >> 16) : (old & 0xFFFFu);
+            S.occ[S.occoff[x] + idx] = (uint16_t)c;
+        }
+    }
+    wave_sync();
+    for (int v = ln; v <= n; v += 64) S.claim[v] = NO_CLAIM;
+    wave_sync();
+
     int trail_len = 0;
     if (nin > 0) {   // caller-supplied dict: later keys overwrite the value, keep their slot
         int tl = 0;
@@ -364,31 +537,36 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
         trail_len = uniform_i32(tl);
         wave_sync();
     }
+    // root snapshot: the input's unit clauses in order; does the input hold `[]`?
     bool has_empty = false;
+    int nu = 0;
     for (int c0 = 0; c0 < m; c0 += 64) {
         const int c = c0 + ln;
-        const bool e = c < m && S.coff[c + 1] == S.coff[c];
-        if (__ballot(e)) has_empty = true;
+        int len = -1;
+        if (c < m) len = S.coff[c + 1] - S.coff[c];
+        if (__ballot(len == 0)) has_empty = true;
+        const uint64_t mk = __ballot(len == 1);
+        if (len == 1) S.units[nu + __popcll(mk & lt)] = S.lit[S.coff[c]];
+        nu += __popcll(mk);
     }
+    wave_sync();
 
     const bool sound = A.mode == SATMI_MODE_SOUND;
     int64_t nodes = 1, decisions = 0, props = 0, pures = 0, conflicts = 0, sols = 0, rounds = 0;
-    int depth = 0, nu = 0;
+    int depth = 0, nsat = 0;
     int status = SATMI_DPLL_EXHAUSTED;
     bool decision_round = false, at_root = true;
-    int state = ST_PROP_SCAN;
+    int state = ST_PROPAGATE;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 
     while (state != ST_DONE) {
-        if (state == ST_PROP_SCAN || state == ST_PROP_PENDING) {
-            int exact_len = trail_len;
-            const bool conflict = propagate(S, m, has_empty, trail_len, nu, state == ST_PROP_SCAN,
-                                            decision_round, props, rounds, &exact_len);
+        if (state == ST_PROPAGATE) {
+            const bool conflict = propagate(S, m, has_empty, trail_len, nu, decision_round, props, rounds, nsat);
             decision_round = false;
             if (at_root) {
                 at_root = false;
-                if (A.root_lits) store_assignment(S, exact_len, A.root_lits + (int64_t)b * A.sol_stride);
-                if (A.root_len && ln == 0) A.root_len[b] = exact_len;
+                if (A.root_lits) store_assignment(S, trail_len, A.root_lits + (int64_t)b * A.sol_stride);
+                if (A.root_len && ln == 0) A.root_len[b] = trail_len;
             }
             if (conflict) {
                 ++conflicts;
@@ -399,17 +577,22 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
             continue;
         }
         if (state == ST_ANALYZE) {
-            const AnRes r = analyze(S, m, n);
             bool leaf = false;
-            if (r.nactive == 0) {
+            AnRes r{0, 0u};
+            if (nsat == m) {
                 leaf = true;                                  // REF.py:170-171
-            } else if (r.npure > 0) {                         // REF.py:186-195
+            } else {
+                r = analyze(S, n);
+                if (r.npure == 0 && r.best_var == 0) leaf = true;   // REF.py:205-206
+            }
+            if (!leaf && r.npure > 0) {                       // REF.py:186-195
+                const int before = trail_len;
                 trail_len = assign_pures(S, L, trail_len);
+                int none = 0;   // a pure literal never empties a clause
+                nsat += apply_range<false>(S, before, trail_len, &none);
                 pures += r.npure;
                 ++nodes;                                      // recursive call; its unit_propagate is a no-op
-            } else if (r.best_var == 0) {
-                leaf = true;                                  // REF.py:205-206
-            } else {                                          // REF.py:208-213
+            } else if (!leaf) {                               // REF.py:208-213
                 const uint32_t v = r.best_var;
                 if (ln == 0) {
                     S.fvar[depth] = (uint16_t)v;
@@ -423,7 +606,7 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                     if (ln == 0) S.units[0] = (uint16_t)code;
                     nu = 1;
                     decision_round = true;
-                    state = ST_PROP_PENDING;
+                    state = ST_PROPAGATE;
                 } else {
                     if (ln == 0) {
                         S.vst[v] = VS_ASSIGNED | VS_VALUE;
@@ -454,8 +637,7 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                 const int top = depth - 1;
                 const uint32_t fv = uniform_u32(S.fvar[top]);
                 const int ft = uniform_i32(S.ftrail[top]);
-                for (int i = ft + ln; i < trail_len; i += 64) S.vst[S.trail[i] >> 1] = 0;
-                wave_sync();
+                unassign_to(S, ft, trail_len, nsat);
                 trail_len = ft;
                 if (!(fv & PHASE_BIT)) {
                     const uint32_t v = fv;
@@ -467,7 +649,7 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                         if (ln == 0) S.units[0] = (uint16_t)code;
                         nu = 1;
                         decision_round = true;
-                        state = ST_PROP_PENDING;
+                        state = ST_PROPAGATE;
                     } else {
                         if (ln == 0) {
                             S.vst[v] = VS_ASSIGNED;
@@ -514,14 +696,17 @@ __global__ void __launch_bounds__(256) dpll_batch_kernel(DpllArgs A) {
     Lds S;
     S.lit = (uint16_t *)(base + A.lay.lit);
     S.coff = (uint16_t *)(base + A.lay.coff);
+    S.occoff = (uint16_t *)(base + A.lay.occoff);
+    S.occ = (uint16_t *)(base + A.lay.occ);
+    S.cst = (uint32_t *)(base + A.lay.cst);
     S.vst = (uint32_t *)(base + A.lay.vst);
+    S.cnt = (uint32_t *)(base + A.lay.cnt);
+    S.claim = (uint32_t *)(base + A.lay.claim);
     S.trail = (uint16_t *)(base + A.lay.trail);
     S.fvar = (uint16_t *)(base + A.lay.fvar);
     S.ftrail = (uint16_t *)(base + A.lay.ftrail);
     S.units = (uint16_t *)(base + A.lay.units);
-    S.cnt = (uint32_t *)(base + A.lay.cnt);
-    S.first = (uint32_t *)(base + A.lay.first);
-    S.sgn = (uint32_t *)(base + A.lay.sgn);
+    S.ubits = (uint64_t *)(base + A.lay.ubits);
     S.posbits = (uint64_t *)(base + A.lay.posbits);
     for (;;) {
         uint32_t b = 0;
@@ -538,19 +723,23 @@ static uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
 static bool make_layout(int max_vars, int max_clauses, int max_lits, DpllLayout *lay) {
     if (max_vars < 0 || max_clauses < 0 || max_lits < 0) return false;
-    if (max_vars > 32767 || max_clauses > 65534 || max_lits > 65535) return false;
+    // 16-bit literal codes, clause indices, literal positions and per-clause counts
+    if (max_vars > 32766 || max_clauses > 65534 || max_lits > 65535) return false;
     const uint32_t N = (uint32_t)max_vars + 1, M = (uint32_t)max_clauses + 1, Lc = (uint32_t)max_lits + 1;
     uint32_t o = 0;
     lay->lit = o;     o = align16(o + 2 * Lc);
     lay->coff = o;    o = align16(o + 2 * M);
+    lay->occoff = o;  o = align16(o + 2 * (2 * N + 1));
+    lay->occ = o;     o = align16(o + 2 * Lc);
+    lay->cst = o;     o = align16(o + 4 * M);
     lay->vst = o;     o = align16(o + 4 * N);
+    lay->cnt = o;     o = align16(o + 4 * N);
+    lay->claim = o;   o = align16(o + 4 * N);
     lay->trail = o;   o = align16(o + 2 * N);
     lay->fvar = o;    o = align16(o + 2 * N);
     lay->ftrail = o;  o = align16(o + 2 * N);
     lay->units = o;   o = align16(o + 2 * M);
-    lay->cnt = o;     o = align16(o + 4 * N);
-    lay->first = o;   o = align16(o + 4 * N);
-    lay->sgn = o;     o = align16(o + 4 * N);
+    lay->ubits = o;   o = align16(o + 8 * ((M + 63) / 64));
     lay->posbits = o; o = align16(o + 8 * ((Lc + 63) / 64));
     lay->bytes = o;
     lay->lcap = max_lits;
@@ -627,9 +816,19 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
     DeviceWork *w = nullptr;
     int rc = device_work(&w);
     if (rc) return rc;
-    const int waves_per_wg = lay.bytes * 4 <= 160u * 1024u ? 4 : (lay.bytes * 2 <= 160u * 1024u ? 2 : 1);
+    // Occupancy is set by LDS: pick the workgroup shape that keeps the most
+    // waves resident (<= 32 waves and, conservatively, <= 16 workgroups per CU).
+    int waves_per_wg = 1, wg_per_cu = 1, best_waves = 0;
+    for (int wpg : {4, 2, 1}) {
+        const int wgs = std::min(16, (int)((160u * 1024u) / (lay.bytes * (uint32_t)wpg)));
+        const int waves = std::min(32, wgs * wpg);
+        if (wgs >= 1 && waves > best_waves) {
+            best_waves = waves;
+            waves_per_wg = wpg;
+            wg_per_cu = std::max(1, std::min(wgs, 32 / wpg));
+        }
+    }
     const uint32_t wg_lds = lay.bytes * (uint32_t)waves_per_wg;
-    const int wg_per_cu = std::max(1, std::min(8, (int)((160u * 1024u) / wg_lds)));
     int dev = 0, cus = 256;
     SATMI_HIP(hipGetDevice(&dev));
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;

@@ -113,8 +113,12 @@ def test_edge_cases():
 
 
 def test_limits_and_too_large():
-    f = cnf.uniform_ksat(1, 40, 40, 3, seed=1).instance(0)
-    r = dpll_batch([f], mode="ref", max_solutions=0, node_limit=100, sol_cap=4)
+    f = cnf.uniform_ksat(1, 40, 170, 3, seed=1).instance(0)
+    o = oracle.dpll(f, "ref", node_limit=50, sol_cap=4)
+    assert o["status"] == 2
+    r = dpll_batch([f], mode="ref", max_solutions=0, node_limit=50, sol_cap=4)
     assert r.status[0] == _capi.DPLL_NODE_LIMIT
-    r = dpll_batch([f], mode="ref", max_solutions=0, time_limit=0.05, sol_cap=4)
+    assert r.counter_dict(0)["nodes"] == 51
+    hard = cnf.uniform_ksat(1, 250, 1065, 3, seed=3).instance(0)
+    r = dpll_batch([hard], mode="sound", max_solutions=0, time_limit=0.05, sol_cap=4)
     assert r.status[0] == _capi.DPLL_TIMEOUT
