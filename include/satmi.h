@@ -54,7 +54,7 @@ extern "C" {
 #define SATMI_CTR_CONFLICTS 4    /* unit_propagate returned None (REF.py:168)    */
 #define SATMI_CTR_SOLUTIONS 5    /* solutions found (len of REF.py's result)     */
 #define SATMI_CTR_ROUNDS 6       /* unit-propagation rounds (clause scans)       */
-#define SATMI_CTR_RESERVED 7
+#define SATMI_CTR_TICKS 7        /* wall-clock ticks the wave spent on the instance (100 MHz s_memrealtime) */
 
 int satmi_abi_version(void);
 const char *satmi_last_error(void);

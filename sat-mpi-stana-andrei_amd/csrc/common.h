@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 #include <string>
 
 #include "satmi.h"
@@ -40,31 +41,58 @@ __device__ __forceinline__ uint32_t uniform_u32(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
 }
 
-__device__ __forceinline__ int wave_min_i32(int x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
-    return uniform_i32(x);
-}
+// ---- DPP (GFX9 data-parallel primitives): wave scans / reductions without an
+// LDS round trip.  row_shr:n shifts within 16-lane rows; row_bcast:15 / :31
+// carry a row's last lane into the following row(s).
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118;
+constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
 
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t y = __shfl_xor(x, o, 64);
-        x = x > y ? x : y;
-    }
-    uint32_t lo = uniform_u32((uint32_t)x), hi = uniform_u32((uint32_t)(x >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
+#define SATMI_DPP(old, x, ctrl, rmask) __builtin_amdgcn_update_dpp((old), (x), (ctrl), (rmask), 0xf, false)
 
 // inclusive prefix sum over the 64 lanes
 __device__ __forceinline__ int wave_incl_scan(int x) {
-    const int l = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o, 64);
-        if (l >= o) x += y;
-    }
+    x += SATMI_DPP(0, x, DPP_ROW_SHR1, 0xf);
+    x += SATMI_DPP(0, x, DPP_ROW_SHR2, 0xf);
+    x += SATMI_DPP(0, x, DPP_ROW_SHR4, 0xf);
+    x += SATMI_DPP(0, x, DPP_ROW_SHR8, 0xf);
+    x += SATMI_DPP(0, x, DPP_ROW_BCAST15, 0xa);
+    x += SATMI_DPP(0, x, DPP_ROW_BCAST31, 0xc);
     return x;
+}
+
+// inclusive prefix max over the 64 lanes
+__device__ __forceinline__ int wave_incl_max(int x) {
+    x = max(x, SATMI_DPP(INT_MIN, x, DPP_ROW_SHR1, 0xf));
+    x = max(x, SATMI_DPP(INT_MIN, x, DPP_ROW_SHR2, 0xf));
+    x = max(x, SATMI_DPP(INT_MIN, x, DPP_ROW_SHR4, 0xf));
+    x = max(x, SATMI_DPP(INT_MIN, x, DPP_ROW_SHR8, 0xf));
+    x = max(x, SATMI_DPP(INT_MIN, x, DPP_ROW_BCAST15, 0xa));
+    x = max(x, SATMI_DPP(INT_MIN, x, DPP_ROW_BCAST31, 0xc));
+    return x;
+}
+
+__device__ __forceinline__ int lane63(int x) { return __builtin_amdgcn_readlane(x, 63); }
+
+// wave-uniform reductions (all 64 lanes must be active)
+__device__ __forceinline__ int wave_min_i32(int x) {
+    x = min(x, SATMI_DPP(INT_MAX, x, DPP_ROW_SHR1, 0xf));
+    x = min(x, SATMI_DPP(INT_MAX, x, DPP_ROW_SHR2, 0xf));
+    x = min(x, SATMI_DPP(INT_MAX, x, DPP_ROW_SHR4, 0xf));
+    x = min(x, SATMI_DPP(INT_MAX, x, DPP_ROW_SHR8, 0xf));
+    x = min(x, SATMI_DPP(INT_MAX, x, DPP_ROW_BCAST15, 0xa));
+    x = min(x, SATMI_DPP(INT_MAX, x, DPP_ROW_BCAST31, 0xc));
+    return lane63(x);
+}
+
+__device__ __forceinline__ int wave_max_i32(int x) { return lane63(wave_incl_max(x)); }
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    // order-preserving map of u32 onto i32
+    return (uint32_t)wave_min_i32((int)(x ^ 0x80000000u)) ^ 0x80000000u;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    return (uint32_t)wave_max_i32((int)(x ^ 0x80000000u)) ^ 0x80000000u;
 }
 
 }  // namespace satmi

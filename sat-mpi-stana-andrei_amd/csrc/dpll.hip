@@ -52,11 +52,43 @@ namespace satmi {
 constexpr uint32_t VS_ASSIGNED = 1u, VS_VALUE = 2u, VS_EFF = 4u, VS_FLAGS = 7u;
 constexpr int VS_TIME_SHIFT = 3;
 constexpr uint32_t PHASE_BIT = 0x8000u;
-constexpr uint32_t CST_TRUE1 = 0x10000u;   // one true literal occurrence in cst
+// cst[c] = nfree | ntrue << 8 | (sum of the free literal codes mod 2^16) << 16:
+// when nfree == 1 the high half is the one free literal (clauses <= 255 literals)
+constexpr uint32_t CST_TRUE1 = 0x100u;
+constexpr uint32_t CST_NFREE = 0xFFu;
+constexpr int MAX_CLAUSE_LEN = 255;
 constexpr uint32_t NO_CLAIM = 0xFFFFFFFFu;
 
+// Diagnostic build only (make diag -> libsatmi_diag.so): per-phase shader-clock
+// accounting, written as int64 over the caller's root_lits rows.  The product
+// library compiles every stamp away.
+#ifdef SATMI_PHASE_STAMPS
+struct PhaseClock {
+    uint64_t acc[8];
+    uint64_t t;
+    __device__ void start() {
+        for (int i = 0; i < 8; ++i) acc[i] = 0;
+        t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ void mark(int i) {
+        const uint64_t x = __builtin_amdgcn_s_memtime();
+        acc[i] += x - t;
+        t = x;
+    }
+};
+#define PH_MARK(i) ph.mark(i)
+#else
+struct PhaseClock {
+    __device__ void start() {}
+    __device__ void mark(int) {}
+};
+#define PH_MARK(i) ((void)0)
+#endif
+enum { PH_STAGE = 0, PH_ASSIGN = 1, PH_APPLY = 2, PH_COLLECT = 3, PH_ANALYZE = 4, PH_PURE = 5, PH_BACKTRACK = 6,
+       PH_OTHER = 7 };
+
 struct DpllLayout {
-    uint32_t lit, coff, occoff, occ, cst, vst, cnt, claim, trail, fvar, ftrail, units, ubits, posbits, bytes;
+    uint32_t lit, coff, occoff, occ, cst, vst, cnt, claim, trail, fvar, ftrail, units, ubits, posbits, mark, bytes;
     int32_t lcap, mcap, ncap;
 };
 
@@ -89,7 +121,7 @@ struct Lds {
     uint16_t *coff;     // [mcap+1]    clause offsets into lit
     uint16_t *occoff;   // [2ncap+3]   occurrence-list offsets per literal code
     uint16_t *occ;      // [lcap]      clause index of every occurrence, grouped by literal code
-    uint32_t *cst;      // [mcap]      nfree | ntrue << 16
+    uint32_t *cst;      // [mcap]      nfree | ntrue << 8 | free-literal code sum << 16
     uint32_t *vst;      // [ncap+1]    assigned / value / effective bits, batch time + 1 above bit 3
     uint32_t *cnt;      // [ncap+1]    occurrences in active clauses: positive | negative << 16
     uint32_t *claim;    // [ncap+1]    first snapshot index claiming the variable (scratch)
@@ -99,100 +131,144 @@ struct Lds {
     uint16_t *units;    // [mcap+1]    current unit-clause snapshot (literal codes)
     uint64_t *ubits;    // [mcap/64]   clauses that became unit in the current batch
     uint64_t *posbits;  // [lcap/64]   pure literals by first position
+    int32_t *mark;      // [64]        scratch row (range starts of a flattened apply)
 };
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
-    return uniform_u32(x);
+__device__ __forceinline__ uint32_t cst_ntrue(uint32_t s) { return (s >> 8) & 0xFFu; }
+
+// Time stamp of the clause's emptying: the latest batch time among its (all
+// false) literals.
+__device__ int emptied_time(const Lds &S, uint32_t c) {
+    int t = -1;
+    const int je = S.coff[c + 1];
+    for (int j = S.coff[c]; j < je; ++j) t = max(t, (int)(S.vst[S.lit[j] >> 1] >> VS_TIME_SHIFT) - 1);
+    return t;
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
-    return uniform_u32(x);
-}
-
-// Apply (UNDO=false) or revert (UNDO=true) the effective assignments trail[beg, end):
-// clauses containing the literal gain/lose a true occurrence, clauses containing
-// its negation lose/regain a free occurrence.  All occurrences of the range are
-// processed by the wave at once.  Returns the change in the number of satisfied
-// clauses; for an apply, *e_min receives the earliest batch time at which a
-// clause was emptied (INT_MAX: none) and newly-unit clauses are flagged in ubits.
+// A clause leaves (UNDO: re-enters) the reduced formula: its literals' active
+// occurrence counts change.  Loads are grouped so they overlap.
 template <bool UNDO>
-__device__ int apply_range(const Lds &S, int beg, int end, int *e_min) {
-    const int ln = lane_id();
-    int dsat = 0;
-    int e_loc = INT_MAX;
-    for (int e0 = beg; e0 < end; e0 += 64) {
-        const int e = e0 + ln;
-        int b0 = 0, n0 = 0, b1 = 0, len = 0;
-        if (e < end) {
-            const uint32_t code = S.trail[e];
-            if (!UNDO || (S.vst[code >> 1] & VS_EFF)) {
-                b0 = S.occoff[code];
-                n0 = S.occoff[code + 1] - b0;
-                b1 = S.occoff[code ^ 1u];
-                len = n0 + (S.occoff[(code ^ 1u) + 1] - b1);
+__device__ __forceinline__ void clause_counts(const Lds &S, uint32_t c) {
+    const int jb = S.coff[c], je = S.coff[c + 1];
+    for (int j = jb; j < je; j += 4) {
+        uint32_t x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = (j + u < je) ? (uint32_t)S.lit[j + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (j + u < je) {
+                const uint32_t inc = (x[u] & 1u) ? 0x10000u : 1u;
+                if (UNDO) atomicAdd(&S.cnt[x[u] >> 1], inc);
+                else atomicSub(&S.cnt[x[u] >> 1], inc);
             }
         }
+    }
+}
+
+// One occurrence of literal `code` (r < n0: in its own list, else in its
+// negation's list).  Returns true when the clause changed satisfied state.
+template <bool UNDO>
+__device__ __forceinline__ bool occ_step(const Lds &S, int r, int n0, int b0, int b1, uint32_t code, int &e_loc) {
+    if (r < n0) {   // the literal becomes true (undo: unassigned) in clause c
+        const uint32_t c = S.occ[b0 + r];
+        const uint32_t old = UNDO ? atomicSub(&S.cst[c], CST_TRUE1) : atomicAdd(&S.cst[c], CST_TRUE1);
+        const bool trans = cst_ntrue(old) == (UNDO ? 1u : 0u);
+        if (trans) clause_counts<UNDO>(S, c);
+        return trans;
+    }
+    // -literal becomes false in clause c: one free occurrence less, its code leaves the sum
+    const uint32_t c = S.occ[b1 + (r - n0)];
+    const uint32_t delta = 1u + ((code ^ 1u) << 16);
+    if (UNDO) {
+        atomicAdd(&S.cst[c], delta);
+        return false;
+    }
+    const uint32_t old = atomicSub(&S.cst[c], delta);
+    const uint32_t nf = (old & CST_NFREE) - 1u;
+    if (nf == 0u) {
+        e_loc = min(e_loc, emptied_time(S, c));
+    } else if (nf == 1u && cst_ntrue(old) == 0u) {
+        atomicOr((unsigned long long *)&S.ubits[c >> 6], 1ull << (c & 63));
+    }
+    return false;
+}
+
+// Apply (UNDO=false) or revert (UNDO=true) the effective assignment of up to 64
+// literals held one per lane (`has`), lane order = time order: clauses
+// containing the literal gain/lose a true occurrence, clauses containing its
+// negation lose/regain a free occurrence.  The occurrences of all lanes are
+// flattened over the wave (prefix sum of list lengths; each flat slot finds
+// its owner lane by marking range starts and a max-scan).  Returns the change
+// in the number of satisfied clauses; on apply, e_loc collects the time stamps
+// of emptied clauses and newly-unit clauses are flagged in ubits.
+template <bool UNDO>
+__device__ int apply_lanes(const Lds &S, bool has, uint32_t code, int &e_loc) {
+    const int ln = lane_id();
+    int b0 = 0, n0 = 0, b1 = 0, len = 0;
+    if (has) {
+        b0 = S.occoff[code];
+        n0 = S.occoff[code + 1] - b0;
+        b1 = S.occoff[code ^ 1u];
+        len = n0 + (S.occoff[(code ^ 1u) + 1] - b1);
+    }
+    const uint64_t hm = __ballot(len > 0);
+    int dsat = 0;
+    if (hm == 0ull) return 0;
+    if ((hm & (hm - 1ull)) == 0ull) {   // a single literal: its slots map onto lanes directly
+        const int o = __ffsll((unsigned long long)hm) - 1;
+        const int on0 = __builtin_amdgcn_readlane(n0, o), ob0 = __builtin_amdgcn_readlane(b0, o);
+        const int ob1 = __builtin_amdgcn_readlane(b1, o), olen = __builtin_amdgcn_readlane(len, o);
+        const uint32_t ocode = (uint32_t)__builtin_amdgcn_readlane((int)code, o);
+        for (int f0 = 0; f0 < olen; f0 += 64) {
+            const int f = f0 + ln;
+            bool trans = false;
+            if (f < olen) trans = occ_step<UNDO>(S, f, on0, ob0, ob1, ocode, e_loc);
+            dsat += __popcll(__ballot(trans));
+        }
+    } else {
         const int incl = wave_incl_scan(len);
         const int start = incl - len;
-        const int total = __shfl(incl, 63, 64);
+        const int total = lane63(incl);
+        int carry = 0;
         for (int f0 = 0; f0 < total; f0 += 64) {
             const int f = f0 + ln;
-            // owner = last lane whose range starts at or before f
-            int o = 0;
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1) {
-                const int s = __shfl(start, o + step, 64);
-                if (s <= f) o += step;
-            }
+            S.mark[ln] = -1;
+            wave_sync();
+            if (len > 0 && start >= f0 && start < f0 + 64) S.mark[start - f0] = ln;
+            wave_sync();
+            int o = S.mark[ln];
+            if (ln == 0) o = max(o, carry);
+            o = wave_incl_max(o);
+            carry = lane63(o);
             const int r = f - __shfl(start, o, 64);
             const int on0 = __shfl(n0, o, 64);
             const int ob0 = __shfl(b0, o, 64);
             const int ob1 = __shfl(b1, o, 64);
+            const uint32_t ocode = (uint32_t)__shfl((int)code, o, 64);
             bool trans = false;
-            if (f < total) {
-                if (r < on0) {
-                    const uint32_t c = S.occ[ob0 + r];
-                    const uint32_t old = UNDO ? atomicSub(&S.cst[c], CST_TRUE1) : atomicAdd(&S.cst[c], CST_TRUE1);
-                    trans = (old >> 16) == (UNDO ? 1u : 0u);
-                    if (trans) {   // the clause leaves (re-enters) the reduced formula
-                        const int je = S.coff[c + 1];
-                        for (int j = S.coff[c]; j < je; ++j) {
-                            const uint32_t x = S.lit[j];
-                            const uint32_t inc = (x & 1u) ? 0x10000u : 1u;
-                            if (UNDO) atomicAdd(&S.cnt[x >> 1], inc);
-                            else atomicSub(&S.cnt[x >> 1], inc);
-                        }
-                    }
-                } else {
-                    const uint32_t c = S.occ[ob1 + (r - on0)];
-                    if (UNDO) {
-                        atomicAdd(&S.cst[c], 1u);
-                    } else {
-                        const uint32_t old = atomicSub(&S.cst[c], 1u);
-                        const uint32_t nf = (old & 0xFFFFu) - 1u;
-                        if (nf == 0u) {
-                            // emptied: at the latest time stamp among its (all false) literals
-                            int t = -1;
-                            const int je = S.coff[c + 1];
-                            for (int j = S.coff[c]; j < je; ++j)
-                                t = max(t, (int)(S.vst[S.lit[j] >> 1] >> VS_TIME_SHIFT) - 1);
-                            e_loc = min(e_loc, t);
-                        } else if (nf == 1u && (old >> 16) == 0u) {
-                            atomicOr((unsigned long long *)&S.ubits[c >> 6], 1ull << (c & 63));
-                        }
-                    }
-                }
-            }
+            if (f < total) trans = occ_step<UNDO>(S, r, on0, ob0, ob1, ocode, e_loc);
             dsat += __popcll(__ballot(trans));
         }
     }
     wave_sync();
-    if (!UNDO) *e_min = wave_min_i32(e_loc);
     return UNDO ? -dsat : dsat;
+}
+
+// apply_lanes over trail[beg, end) (UNDO: only the effective entries).
+template <bool UNDO>
+__device__ int apply_trail(const Lds &S, int beg, int end) {
+    int dsat = 0, e_loc = INT_MAX;
+    for (int e0 = beg; e0 < end; e0 += 64) {
+        const int e = e0 + lane_id();
+        bool has = false;
+        uint32_t code = 0;
+        if (e < end) {
+            code = S.trail[e];
+            has = !UNDO || (S.vst[code >> 1] & VS_EFF);
+        }
+        dsat += apply_lanes<UNDO>(S, has, code, e_loc);
+    }
+    return dsat;
 }
 
 __device__ void clear_ubits(const Lds &S, int m) {
@@ -201,7 +277,7 @@ __device__ void clear_ubits(const Lds &S, int m) {
 }
 
 // The next snapshot: clauses flagged in ubits that are still unit, in clause
-// order (REF.py:143), each represented by its one free literal.
+// order (REF.py:143); cst's high half holds the one free literal's code.
 __device__ int collect_units(const Lds &S, int m) {
     const int ln = lane_id();
     const int W = (m + 63) >> 6;
@@ -216,25 +292,16 @@ __device__ int collect_units(const Lds &S, int m) {
         uint64_t keep = 0;
         for (uint64_t b = bits; b; b &= b - 1) {
             const int c = w * 64 + (__ffsll((unsigned long long)b) - 1);
-            if (S.cst[c] == 1u) keep |= b & (~b + 1);   // ntrue == 0 and nfree == 1
+            if ((S.cst[c] & 0xFFFFu) == 1u) keep |= b & (~b + 1);   // nfree == 1, ntrue == 0
         }
         const int kc = __popcll(keep);
         const int incl = wave_incl_scan(kc);
         int pos = nu + incl - kc;
         for (; keep; keep &= keep - 1) {
             const int c = w * 64 + (__ffsll((unsigned long long)keep) - 1);
-            uint32_t code = 0;
-            const int je = S.coff[c + 1];
-            for (int j = S.coff[c]; j < je; ++j) {
-                const uint32_t x = S.lit[j];
-                if (!(S.vst[x >> 1] & VS_EFF)) {
-                    code = x;
-                    break;
-                }
-            }
-            S.units[pos++] = (uint16_t)code;
+            S.units[pos++] = (uint16_t)(S.cst[c] >> 16);
         }
-        nu += __shfl(incl, 63, 64);
+        nu += lane63(incl);
     }
     wave_sync();
     return uniform_i32(nu);
@@ -244,7 +311,7 @@ __device__ int collect_units(const Lds &S, int m) {
 // true on conflict.  `trail_len` ends at the exact point the reference stops
 // (the assignments it made, including the one that emptied a clause).
 __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, int nu, bool decision_round,
-                          int64_t &props, int64_t &rounds, int &nsat) {
+                          int64_t &props, int64_t &rounds, int &nsat, PhaseClock &ph) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     bool dec = decision_round;
@@ -252,52 +319,46 @@ __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, i
     for (int guard = 0; nu > 0 && guard <= 32768; ++guard) {
         ++rounds;
         const int round_start = trail_len;
-        // (1) variables assigned before this snapshot: equal value -> `continue`,
-        //     different value -> conflict at that unit (REF.py:149-151)
-        int kmis = INT_MAX;
-        for (int k0 = 0; k0 < nu; k0 += 64) {
+        int kmis = INT_MAX, e_min = INT_MAX, first_k = INT_MAX;
+        uint32_t code = 0;
+        bool first = false;
+        for (int k0 = 0; k0 < nu && kmis == INT_MAX && e_min == INT_MAX; k0 += 64) {
             const int k = k0 + ln;
-            if (k < nu) {
-                const uint32_t code = S.units[k];
-                const uint32_t s = S.vst[code >> 1];
-                if (s & VS_ASSIGNED) {
-                    if (((s >> 1) & 1u) == (code & 1u)) kmis = min(kmis, k);
-                } else {
-                    atomicMin(&S.claim[code >> 1], (uint32_t)k);
-                }
-            }
-        }
-        kmis = wave_min_i32(kmis);
-        wave_sync();
-        // (2) the first occurrence of each variable before the mismatch is assigned,
-        //     in snapshot order, time-stamped with its snapshot index (REF.py:154)
-        const int lim = min(nu, kmis);
-        int nassign = 0, first_k = INT_MAX;
-        for (int k0 = 0; k0 < lim; k0 += 64) {
-            const int k = k0 + ln;
-            bool first = false;
-            uint32_t code = 0;
-            if (k < lim) {
-                code = S.units[k];
-                first = S.claim[code >> 1] == (uint32_t)k;
-            }
+            const bool valid = k < nu;
+            code = valid ? (uint32_t)S.units[k] : 0u;
+            const uint32_t v = code >> 1;
+            const uint32_t s = valid ? S.vst[v] : 0u;
+            const bool assigned = (s & VS_ASSIGNED) != 0u;
+            // assigned before this snapshot (no time stamp): equal value -> `continue`,
+            // different value -> conflict at this unit (REF.py:149-151)
+            const bool mis = valid && assigned && (s >> VS_TIME_SHIFT) == 0u && ((s >> 1) & 1u) == (code & 1u);
+            kmis = wave_min_i32(mis ? k : INT_MAX);
+            // the first occurrence of each unassigned variable before the mismatch
+            // is assigned, time-stamped with its snapshot index (REF.py:154)
+            const bool claimable = valid && !assigned && k < kmis;
+            if (claimable) atomicMin(&S.claim[v], (uint32_t)k);
+            wave_sync();
+            first = claimable && S.claim[v] == (uint32_t)k;
+            wave_sync();
+            if (claimable) S.claim[v] = NO_CLAIM;
             const uint64_t mk = __ballot(first);
             if (first) {
-                S.trail[trail_len + nassign + __popcll(mk & lt)] = (uint16_t)code;
-                S.vst[code >> 1] = VS_ASSIGNED | VS_EFF | ((code & 1u) ? 0u : VS_VALUE) |
-                                   ((uint32_t)(k + 1) << VS_TIME_SHIFT);
+                S.trail[trail_len + __popcll(mk & lt)] = (uint16_t)code;
+                S.vst[v] = VS_ASSIGNED | VS_EFF | ((code & 1u) ? 0u : VS_VALUE) |
+                           ((uint32_t)(k + 1) << VS_TIME_SHIFT);
             }
             if (mk && first_k == INT_MAX) first_k = k0 + __ffsll((unsigned long long)mk) - 1;
-            nassign += __popcll(mk);
+            trail_len += __popcll(mk);
+            wave_sync();
+            PH_MARK(PH_ASSIGN);
+            // reduce the formula by this part of the batch (REF.py:156-164)
+            int e_loc = INT_MAX;
+            nsat += apply_lanes<false>(S, first, code, e_loc);
+            e_min = wave_min_i32(e_loc);
+            if (has_empty && mk) e_min = min(e_min, first_k);   // `[]` empties at the first reduction
+            PH_MARK(PH_APPLY);
         }
-        wave_sync();
-        for (int k = ln; k < nu; k += 64) S.claim[S.units[k] >> 1] = NO_CLAIM;
-        trail_len += nassign;
-        wave_sync();
-        // (3) reduce the formula by the batch (REF.py:156-164)
-        int e_min = INT_MAX;
-        nsat += apply_range<false>(S, round_start, trail_len, &e_min);
-        if (has_empty && nassign > 0) e_min = min(e_min, first_k);   // `[]` empties at the first reduction
+        const int nassign = trail_len - round_start;
         if (e_min != INT_MAX) {
             // the reference stopped at the unit with time stamp e_min: undo the rest
             int keep = 0;
@@ -308,7 +369,7 @@ __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, i
                 keep += __popcll(__ballot(p));
             }
             const int cut = round_start + keep;
-            nsat += apply_range<true>(S, cut, trail_len, nullptr);
+            nsat += apply_trail<true>(S, cut, trail_len);
             for (int i = round_start + ln; i < trail_len; i += 64) {
                 const uint32_t v = S.trail[i] >> 1;
                 S.vst[v] = i < cut ? (S.vst[v] & VS_FLAGS) : 0u;
@@ -320,7 +381,12 @@ __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, i
         }
         props += nassign - (dec && nassign > 0 ? 1 : 0);
         dec = false;
-        for (int i = round_start + ln; i < trail_len; i += 64) S.vst[S.trail[i] >> 1] &= VS_FLAGS;
+        // drop this batch's time stamps
+        if (nu <= 64) {
+            if (first) S.vst[code >> 1] = VS_ASSIGNED | VS_EFF | ((code & 1u) ? 0u : VS_VALUE);
+        } else {
+            for (int i = round_start + ln; i < trail_len; i += 64) S.vst[S.trail[i] >> 1] &= VS_FLAGS;
+        }
         wave_sync();
         if (kmis != INT_MAX) {
             clear_ubits(S, m);
@@ -328,20 +394,26 @@ __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, i
         }
         if (nassign == 0) break;   // `changed` stayed False (REF.py:141-142)
         nu = collect_units(S, m);
+        PH_MARK(PH_COLLECT);
     }
     return false;
 }
 
 // First occurrence of variable v in the reduced formula (position in lit), the
 // key of literal_sign / var_counts' dict order (REF.py:174-179, :198-203).
-// Requires v to occur in an active clause.
+// Occurrence lists are sorted by clause, so each walk stops at its first
+// active clause.  Requires v to occur in an active clause.
 __device__ uint32_t first_position(const Lds &S, uint32_t v) {
     uint32_t best = 0xFFFFFFFFu;
     for (uint32_t code = v << 1; code <= ((v << 1) | 1u); ++code) {
         const int e = S.occoff[code + 1];
         for (int i = S.occoff[code]; i < e; ++i) {
             const uint32_t c = S.occ[i];
-            if (c < best && (S.cst[c] >> 16) == 0u) best = c;
+            if (c >= best) break;
+            if (cst_ntrue(S.cst[c]) == 0u) {
+                best = c;
+                break;
+            }
         }
     }
     if (best == 0xFFFFFFFFu) return 0xFFFFFFFFu;
@@ -415,7 +487,7 @@ __device__ int assign_pures(const Lds &S, int L, int trail_len) {
             S.vst[v] = VS_ASSIGNED | VS_EFF | (positive ? VS_VALUE : 0u);
         }
         if (w < W) S.posbits[w] = 0ull;
-        base += __shfl(incl, 63, 64);
+        base += lane63(incl);
     }
     wave_sync();
     return trail_len + uniform_i32(base);
@@ -431,7 +503,7 @@ __device__ void store_assignment(const Lds &S, int trail_len, int32_t *out) {
 
 // Pop trail[ft, trail_len): revert the effective ones, clear every variable.
 __device__ void unassign_to(const Lds &S, int ft, int trail_len, int &nsat) {
-    nsat += apply_range<true>(S, ft, trail_len, nullptr);
+    nsat += apply_trail<true>(S, ft, trail_len);
     for (int i = ft + lane_id(); i < trail_len; i += 64) S.vst[S.trail[i] >> 1] = 0u;
     wave_sync();
 }
@@ -439,6 +511,9 @@ __device__ void unassign_to(const Lds &S, int ft, int trail_len, int &nsat) {
 enum { ST_PROPAGATE = 0, ST_ANALYZE = 1, ST_BACKTRACK = 2, ST_DONE = 3 };
 
 __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    PhaseClock ph;
+    ph.start();
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     const int cb = A.inst_clause_begin[b], ce = A.inst_clause_begin[b + 1];
@@ -475,7 +550,23 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
     for (int w = ln; w < ((m + 63) >> 6); w += 64) S.ubits[w] = 0ull;
     for (int w = ln; w < ((L + 63) >> 6); w += 64) S.posbits[w] = 0ull;
     wave_sync();
-    for (int c = ln; c < m; c += 64) S.cst[c] = (uint32_t)(S.coff[c + 1] - S.coff[c]);
+    // cst = clause length | code sum << 16; clauses longer than 255 literals do not fit
+    bool too_long = false;
+    for (int c = ln; c < m; c += 64) {
+        const int jb = S.coff[c], je = S.coff[c + 1];
+        uint32_t sum = 0;
+        for (int j = jb; j < je; ++j) sum += S.lit[j];
+        too_long |= (je - jb) > MAX_CLAUSE_LEN;
+        S.cst[c] = (uint32_t)(je - jb) | (sum << 16);
+    }
+    if (__ballot(too_long)) {
+        if (ln < SATMI_NCOUNTERS) ctr[ln] = 0;
+        if (ln == 0) {
+            A.status[b] = SATMI_DPLL_TOO_LARGE;
+            if (A.root_len) A.root_len[b] = 0;
+        }
+        return;
+    }
     for (int i = ln; i < L; i += 64) {
         const uint32_t x = S.lit[i];
         atomicAdd(&S.cnt[x >> 1], (x & 1u) ? 0x10000u : 1u);   // all clauses are active
@@ -499,21 +590,43 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                 S.occoff[2 * v] = (uint16_t)o;
                 S.occoff[2 * v + 1] = (uint16_t)(o + (int)p);
             }
-            base += __shfl(incl, 63, 64);
+            base += lane63(incl);
         }
         if (ln == 0) S.occoff[2 * n + 2] = (uint16_t)L;
     }
     wave_sync();
-    for (int c = ln; c < m; c += 64) {
-        const int je = S.coff[c + 1];
-        for (int j = S.coff[c]; j < je; ++j) {
-            const uint32_t x = S.lit[j];
-            const uint32_t old = atomicAdd(&S.claim[x >> 1], (x & 1u) ? 0x10000u : 1u);
-            const uint32_t idx = (x & 1u) ? (old >> 16) : (old & 0xFFFFu);
-            S.occ[S.occoff[x] + idx] = (uint16_t)c;
+    // scatter occurrences in position (= clause) order so every list is sorted by
+    // clause: within a 64-position chunk, equal codes are ranked by lane, the
+    // group's first lane advances the code's cursor (claim[] doubles as cursor)
+    for (int p0 = 0; p0 < L; p0 += 64) {
+        const int p = p0 + ln;
+        const bool valid = p < L;
+        const uint32_t x = valid ? (uint32_t)S.lit[p] : 0xFFFFFFFFu;
+        int rank = 0, grp = 0;
+#pragma unroll 8
+        for (int l = 0; l < 64; ++l) {
+            const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+            const bool eq = y == x;
+            grp += eq ? 1 : 0;
+            rank += (eq && l < ln) ? 1 : 0;
         }
+        const uint32_t unit = (x & 1u) ? 0x10000u : 1u;
+        if (valid && rank == 0) atomicAdd(&S.claim[x >> 1], unit * (uint32_t)grp);
+        wave_sync();
+        if (valid) {
+            const uint32_t cur = S.claim[x >> 1];
+            const int after = (int)((x & 1u) ? (cur >> 16) : (cur & 0xFFFFu));
+            // clause of position p: the last c with coff[c] <= p
+            int lo = 0, hi = m;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if ((int)S.coff[mid] <= p) lo = mid;
+                else hi = mid;
+            }
+            S.occ[S.occoff[x] + after - grp + rank] = (uint16_t)lo;
+        }
+        wave_sync();
     }
-    wave_sync();
     for (int v = ln; v <= n; v += 64) S.claim[v] = NO_CLAIM;
     wave_sync();
 
@@ -551,6 +664,7 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
     }
     wave_sync();
 
+    PH_MARK(PH_STAGE);
     const bool sound = A.mode == SATMI_MODE_SOUND;
     int64_t nodes = 1, decisions = 0, props = 0, pures = 0, conflicts = 0, sols = 0, rounds = 0;
     int depth = 0, nsat = 0;
@@ -561,7 +675,7 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
 
     while (state != ST_DONE) {
         if (state == ST_PROPAGATE) {
-            const bool conflict = propagate(S, m, has_empty, trail_len, nu, decision_round, props, rounds, nsat);
+            const bool conflict = propagate(S, m, has_empty, trail_len, nu, decision_round, props, rounds, nsat, ph);
             decision_round = false;
             if (at_root) {
                 at_root = false;
@@ -585,13 +699,14 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                 r = analyze(S, n);
                 if (r.npure == 0 && r.best_var == 0) leaf = true;   // REF.py:205-206
             }
+            PH_MARK(PH_ANALYZE);
             if (!leaf && r.npure > 0) {                       // REF.py:186-195
                 const int before = trail_len;
                 trail_len = assign_pures(S, L, trail_len);
-                int none = 0;   // a pure literal never empties a clause
-                nsat += apply_range<false>(S, before, trail_len, &none);
+                nsat += apply_trail<false>(S, before, trail_len);   // a pure literal never empties a clause
                 pures += r.npure;
                 ++nodes;                                      // recursive call; its unit_propagate is a no-op
+                PH_MARK(PH_PURE);
             } else if (!leaf) {                               // REF.py:208-213
                 const uint32_t v = r.best_var;
                 if (ln == 0) {
@@ -663,6 +778,7 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                 }
                 --depth;
             }
+            PH_MARK(PH_BACKTRACK);
         }
         if (state != ST_DONE) {
             if (A.node_limit > 0 && nodes > A.node_limit) {
@@ -683,8 +799,13 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
         ctr[SATMI_CTR_CONFLICTS] = conflicts;
         ctr[SATMI_CTR_SOLUTIONS] = sols;
         ctr[SATMI_CTR_ROUNDS] = rounds;
-        ctr[SATMI_CTR_RESERVED] = 0;
+        ctr[SATMI_CTR_TICKS] = (int64_t)(__builtin_amdgcn_s_memrealtime() - t_start);
     }
+#ifdef SATMI_PHASE_STAMPS
+    PH_MARK(PH_OTHER);
+    if (A.root_lits && A.sol_stride >= 16 && ln < 8)
+        ((int64_t *)(A.root_lits + (int64_t)b * A.sol_stride))[ln] = (int64_t)ph.acc[ln];
+#endif
 }
 
 // Persistent grid: every wave pulls instance indices from a global counter until
@@ -708,6 +829,7 @@ __global__ void __launch_bounds__(256) dpll_batch_kernel(DpllArgs A) {
     S.units = (uint16_t *)(base + A.lay.units);
     S.ubits = (uint64_t *)(base + A.lay.ubits);
     S.posbits = (uint64_t *)(base + A.lay.posbits);
+    S.mark = (int32_t *)(base + A.lay.mark);
     for (;;) {
         uint32_t b = 0;
         if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
@@ -741,6 +863,7 @@ static bool make_layout(int max_vars, int max_clauses, int max_lits, DpllLayout 
     lay->units = o;   o = align16(o + 2 * M);
     lay->ubits = o;   o = align16(o + 8 * ((M + 63) / 64));
     lay->posbits = o; o = align16(o + 8 * ((Lc + 63) / 64));
+    lay->mark = o;    o = align16(o + 4 * 64);
     lay->bytes = o;
     lay->lcap = max_lits;
     lay->mcap = max_clauses;

@@ -16,7 +16,7 @@ MODE_REF = 0
 MODE_SOUND = 1
 NCOUNTERS = 8
 COUNTER_NAMES = ("nodes", "decisions", "unit_props", "pure_assigns", "conflicts", "solutions", "rounds",
-                 "reserved")
+                 "ticks")
 DPLL_EXHAUSTED, DPLL_STOPPED, DPLL_NODE_LIMIT, DPLL_TIMEOUT, DPLL_TOO_LARGE = range(5)
 STATUS_NAMES = {0: "exhausted", 1: "stopped", 2: "node_limit", 3: "timeout", 4: "too_large"}
 RES_SAT, RES_UNSAT, RES_LIMIT = 1, 0, -1
