@@ -5,11 +5,11 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 A step = one pass of the hot path (csrc/dpll.hip, SOUND mode, stop at the
-first model: the SAT/UNSAT decision) over one batch of B synthetic uniform
-random 3-SAT instances per GPU, already resident in HBM, followed by the RCCL
-all-reduce of the step's verdict/counter totals.  Instances are sharded across
-ranks with no data-path collective (weak scaling: B instances per GPU per step;
-262,144 in total at 8 GPUs = BASELINE.json configs[2]).
+first model: the SAT/UNSAT decision) over one batch of synthetic uniform random
+3-SAT instances already resident in HBM, followed by the RCCL all-reduce of the
+step's verdict/counter totals.  The batch is BASELINE.json configs[2]: 262,144
+instances of n=100, alpha=4.26 per step, sharded across the ranks with no
+data-path collective (strong scaling: 262,144 / N instances per GPU).
 
 Prints ONE JSON line on rank 0.
 """
@@ -26,6 +26,7 @@ import torch  # noqa: E402  (before libsatmi: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
 from satmi import _capi, cnf  # noqa: E402
+from satmi.shard import shard_range  # noqa: E402
 
 METRIC = "instances solved/sec, random 3-SAT n=100 α=4.26; unit-props/sec; HBM GB/s"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -37,7 +38,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--per-gpu", type=int, default=32768, help="instances per GPU per step")
+    p.add_argument("--total", type=int, default=262144, help="instances per step, all ranks (configs[2])")
     p.add_argument("--n", type=int, default=100)
     p.add_argument("--alpha", type=float, default=4.26)
     p.add_argument("--k", type=int, default=3)
@@ -92,7 +93,9 @@ def main():
     torch.cuda.set_device(dev)
     L = _capi.load()
 
-    B, n, k = args.per_gpu, args.n, args.k
+    n, k = args.n, args.k
+    b0, b1 = shard_range(args.total, world, rank)   # this rank's contiguous shard of the step's batch
+    B = b1 - b0
     m = int(round(args.alpha * n))
     # two distinct resident batches per rank, alternated step to step
     batches = [cnf.uniform_ksat_device(B, n, m, k, seed=args.seed + 1000 * rank + j, device=dev) for j in range(2)]
@@ -117,7 +120,8 @@ def main():
         if evs is not None:
             evs[1].record(stream)
         agg = torch.stack([(counters[:, 5] > 0).sum(), counters[:, 2].sum(), counters[:, 0].sum(),
-                           (status > 1).sum(), (sol_len.to(torch.int64) * 4 + 4 * (counters[:, 5] > 0)).sum()])
+                           (status > 1).sum(), (sol_len.to(torch.int64) * 4 + 4 * (counters[:, 5] > 0)).sum(),
+                           counters[:, 7].sum(), torch.tensor(B, device=dev, dtype=torch.int64)])
         if world > 1:
             dist.all_reduce(agg)   # RCCL: gather verdict/counter totals
         return agg
@@ -130,7 +134,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    totals = torch.zeros(5, dtype=torch.int64, device=dev)
+    totals = torch.zeros(7, dtype=torch.int64, device=dev)
     t0 = time.perf_counter()
     for j in range(args.steps):
         totals += step(j, evs[j])
@@ -146,8 +150,7 @@ def main():
     kms = [a.elapsed_time(b) for a, b in evs]
     kernel_ms = sum(kms) / len(kms)
     tot = totals.tolist()
-    nsat, props, nodes, bad, written = tot
-    all_inst = B * world * args.steps
+    nsat, props, nodes, bad, written, ticks, all_inst = tot
     value = all_inst / elapsed
 
     # correctness spot check outside the timed region: every reported model satisfies its formula
@@ -167,10 +170,19 @@ def main():
 
     # roofline of the dominant kernel: algorithmic bytes per launch / average launch time
     read_bytes = B * (4 * m * k + 4 * m + 4 + 4) + 4
-    write_bytes = B * (4 + 8 * _capi.NCOUNTERS) + written / (world * args.steps)
+    write_bytes = B * (4 + 8 * _capi.NCOUNTERS) + written / all_inst * B
     alg_bytes = read_bytes + write_bytes
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    workload = f"dpll_sound_3sat_n{n}_a{args.alpha}_B{B}"
+    workload = f"dpll_sound_{k}sat_n{n}_a{args.alpha}_B{B}"
+    # resident waves of the persistent grid -> how busy the waves were (tail of the batch)
+    lds = L.satmi_dpll_lds_bytes(n, m, m * k)
+    per_cu = 0
+    for wpg in (4, 2, 1):
+        wgs = min(16, (160 * 1024) // (lds * wpg))
+        if wgs >= 1:
+            per_cu = max(per_cu, min(32, wgs * wpg))
+    resident = min(B, torch.cuda.get_device_properties(dev).multi_processor_count * per_cu)
+    util = ticks / world * 1e-8 / (resident * kernel_ms * 1e-3 * args.steps)
     pmc = load_pmc(workload)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
@@ -179,16 +191,18 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "instances/s", "n_gpus": world, "steps": args.steps,
         "warmup": warm, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+        "scaling": "strong", "vs_baseline": None, "dtype": "int32",
         "data": "synthetic: uniform random k-SAT generated in HBM (seeded), 2 batches alternated",
         "config": {"workload": f"batched DPLL (SOUND mode, first model = SAT/UNSAT decision), random {k}-SAT "
-                               f"n={n} alpha={args.alpha} m={m}, {B} instances per GPU per step "
-                               f"(BASELINE configs[2]: {B * 8} at 8 GPUs)",
-                   "instances_per_gpu": B, "n": n, "m": m, "k": k, "parallelism": f"instance-sharded x{world}"},
+                               f"n={n} alpha={args.alpha} m={m}, {args.total} instances per step sharded over "
+                               f"{world} GPU(s) (BASELINE configs[2])",
+                   "instances_per_step": args.total, "instances_per_gpu": B, "n": n, "m": m, "k": k,
+                   "parallelism": f"instance-sharded x{world}"},
         "unit_props_per_s": props / elapsed,
         "nodes_per_s": nodes / elapsed,
         "sat_fraction": nsat / all_inst,
         "hbm_gbs": achieved,
+        "wave_utilisation": util,
         "roofline": roof,
     }
     if rank == 0:

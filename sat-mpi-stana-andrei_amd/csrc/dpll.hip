@@ -146,51 +146,49 @@ __device__ int emptied_time(const Lds &S, uint32_t c) {
 }
 
 // A clause leaves (UNDO: re-enters) the reduced formula: its literals' active
-// occurrence counts change.  Loads are grouped so they overlap.
+// occurrence counts change.  Slots past the clause end add 0 to cnt[0] (an
+// unused word) so the group of four loads and atomics runs without branches.
 template <bool UNDO>
 __device__ __forceinline__ void clause_counts(const Lds &S, uint32_t c) {
     const int jb = S.coff[c], je = S.coff[c + 1];
     for (int j = jb; j < je; j += 4) {
         uint32_t x[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = (j + u < je) ? (uint32_t)S.lit[j + u] : 0u;
+        for (int u = 0; u < 4; ++u) x[u] = S.lit[j + u];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if (j + u < je) {
-                const uint32_t inc = (x[u] & 1u) ? 0x10000u : 1u;
-                if (UNDO) atomicAdd(&S.cnt[x[u] >> 1], inc);
-                else atomicSub(&S.cnt[x[u] >> 1], inc);
-            }
+            const bool in = j + u < je;
+            const uint32_t inc = in ? ((x[u] & 1u) ? 0x10000u : 1u) : 0u;
+            const uint32_t v = in ? (x[u] >> 1) : 0u;
+            if (UNDO) atomicAdd(&S.cnt[v], inc);
+            else atomicSub(&S.cnt[v], inc);
         }
     }
 }
 
 // One occurrence of literal `code` (r < n0: in its own list, else in its
-// negation's list).  Returns true when the clause changed satisfied state.
+// negation's list), as one atomic on the clause word.  Returns true when the
+// clause changed satisfied state.
 template <bool UNDO>
 __device__ __forceinline__ bool occ_step(const Lds &S, int r, int n0, int b0, int b1, uint32_t code, int &e_loc) {
-    if (r < n0) {   // the literal becomes true (undo: unassigned) in clause c
-        const uint32_t c = S.occ[b0 + r];
-        const uint32_t old = UNDO ? atomicSub(&S.cst[c], CST_TRUE1) : atomicAdd(&S.cst[c], CST_TRUE1);
-        const bool trans = cst_ntrue(old) == (UNDO ? 1u : 0u);
-        if (trans) clause_counts<UNDO>(S, c);
-        return trans;
+    const bool pos = r < n0;
+    const uint32_t c = S.occ[pos ? b0 + r : b1 + (r - n0)];
+    // own list: a true occurrence more (undo: less); negation's list: a free
+    // occurrence less and its code leaves the sum (undo: back)
+    const uint32_t fdelta = 1u + ((code ^ 1u) << 16);
+    const uint32_t delta = pos ? (UNDO ? 0u - CST_TRUE1 : CST_TRUE1) : (UNDO ? fdelta : 0u - fdelta);
+    const uint32_t old = atomicAdd(&S.cst[c], delta);
+    const bool trans = pos && cst_ntrue(old) == (UNDO ? 1u : 0u);
+    if (trans) clause_counts<UNDO>(S, c);
+    if (!UNDO && !pos) {
+        const uint32_t nf = (old & CST_NFREE) - 1u;
+        if (nf == 0u) {
+            e_loc = min(e_loc, emptied_time(S, c));
+        } else if (nf == 1u && cst_ntrue(old) == 0u) {
+            atomicOr((unsigned long long *)&S.ubits[c >> 6], 1ull << (c & 63));
+        }
     }
-    // -literal becomes false in clause c: one free occurrence less, its code leaves the sum
-    const uint32_t c = S.occ[b1 + (r - n0)];
-    const uint32_t delta = 1u + ((code ^ 1u) << 16);
-    if (UNDO) {
-        atomicAdd(&S.cst[c], delta);
-        return false;
-    }
-    const uint32_t old = atomicSub(&S.cst[c], delta);
-    const uint32_t nf = (old & CST_NFREE) - 1u;
-    if (nf == 0u) {
-        e_loc = min(e_loc, emptied_time(S, c));
-    } else if (nf == 1u && cst_ntrue(old) == 0u) {
-        atomicOr((unsigned long long *)&S.ubits[c >> 6], 1ull << (c & 63));
-    }
-    return false;
+    return trans;
 }
 
 // Apply (UNDO=false) or revert (UNDO=true) the effective assignment of up to 64
@@ -849,7 +847,7 @@ static bool make_layout(int max_vars, int max_clauses, int max_lits, DpllLayout 
     if (max_vars > 32766 || max_clauses > 65534 || max_lits > 65535) return false;
     const uint32_t N = (uint32_t)max_vars + 1, M = (uint32_t)max_clauses + 1, Lc = (uint32_t)max_lits + 1;
     uint32_t o = 0;
-    lay->lit = o;     o = align16(o + 2 * Lc);
+    lay->lit = o;     o = align16(o + 2 * (Lc + 4));   // +4: clause_counts reads in groups of four
     lay->coff = o;    o = align16(o + 2 * M);
     lay->occoff = o;  o = align16(o + 2 * (2 * N + 1));
     lay->occ = o;     o = align16(o + 2 * Lc);

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round profile of the benchmark on one MI355X (run through gpurun):
+#   bench line, rocprofv3 kernel-trace stats, and HBM traffic of the DPLL kernel
+#   from separate FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md, HBM section).
+# Usage: bash tools/profile_bench.sh <tag>      -> gpurun_out/<tag>/...
+set -eo pipefail
+TAG=${1:-prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+ROOT=$(pwd)
+export TMPDIR=/tmp
+timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace" -o trace \
+    -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$ROOT/$OUT/fetch" -o fetch \
+    -- python bench.py --steps 2 --warmup 0 --profile-steps > "$OUT/fetch_bench.json" 2> "$OUT/fetch.err"
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$ROOT/$OUT/write" -o write \
+    -- python bench.py --steps 2 --warmup 0 --profile-steps > "$OUT/write_bench.json" 2> "$OUT/write.err"
+echo done
