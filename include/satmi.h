@@ -107,6 +107,25 @@ int satmi_dpll_batch_host(int num_instances, const int32_t *h_inst_clause_begin,
                           int32_t *h_status, int64_t *h_counters, int32_t *h_sol_len,
                           int32_t *h_sol_lits, int32_t *h_root_len, int32_t *h_root_lits);
 
+/*
+ * Resolution saturation, replaces resolution_solver (REF.py:63-95) for one
+ * clause set (CSR host arrays: clause c = lits[clause_off[c] .. clause_off[c+1])).
+ * Clauses are variable bitsets in HBM; each pass resolves all pairs on the GPU
+ * (tautologies filtered), dedups by sort + merge against the sorted `seen` set.
+ *   max_passes / clause_limit / time_limit_s   <= 0: unlimited
+ *   *result   1 = True (no new clause derivable), 0 = False (empty resolvent),
+ *             -1 = a limit stopped the saturation
+ *   *passes   completed passes that added clauses; pass_new[p] = clauses added
+ *   optional record (all three non-NULL): clauses new in pass p are
+ *   rec_pass_off[p] .. rec_pass_off[p+1] in rec_clause_off / rec_lits, each
+ *   clause as ascending literals.
+ */
+int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_lits,
+                          int64_t max_passes, int64_t clause_limit, double time_limit_s,
+                          int32_t *h_result, int32_t *h_passes, int64_t *h_pass_new, int pass_cap,
+                          int32_t *h_rec_lits, int64_t rec_lit_cap, int64_t *h_rec_clause_off,
+                          int64_t rec_clause_cap, int64_t *h_rec_pass_off, int rec_pass_cap);
+
 /* LDS bytes one wavefront needs for an instance of this size (0 = unsupported). */
 uint64_t satmi_dpll_lds_bytes(int max_vars, int max_clauses, int max_lits);
 
