@@ -126,6 +126,24 @@ int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, const int32
                           int32_t *h_rec_lits, int64_t rec_lit_cap, int64_t *h_rec_clause_off,
                           int64_t rec_clause_cap, int64_t *h_rec_pass_off, int rec_pass_cap);
 
+/*
+ * Davis-Putnam elimination, replaces davis_putnam_solver (REF.py:98-130) for one
+ * clause set.  Variables are eliminated in the reference's order (CPython's
+ * `set.pop()` on the variable set, modelled on the device), resolvents are
+ * generated, tautology-filtered and subsumption-filtered on the GPU.
+ *   step_limit / clause_limit / time_limit_s   <= 0: unlimited
+ *   *result   1 = True, 0 = False (empty resolvent), -1 = a limit stopped it
+ *   trace_vars[k] = variable eliminated at step k; *steps = steps run
+ *   optional record (all three non-NULL): the clause list after completed step
+ *   s is rec_step_off[s-1] .. rec_step_off[s] in rec_clause_off / rec_lits,
+ *   every clause in its Python set iteration order; rec_step_off[s] is left
+ *   untouched for a step that ended the elimination.
+ */
+int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_lits, int64_t step_limit,
+                  int64_t clause_limit, double time_limit_s, int32_t *h_result, int32_t *h_trace_vars,
+                  int trace_cap, int32_t *h_steps, int32_t *h_rec_lits, int64_t rec_lit_cap,
+                  int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_step_off, int rec_step_cap);
+
 /* LDS bytes one wavefront needs for an instance of this size (0 = unsupported). */
 uint64_t satmi_dpll_lds_bytes(int max_vars, int max_clauses, int max_lits);
 

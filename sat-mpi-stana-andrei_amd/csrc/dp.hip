@@ -1,0 +1,629 @@
+// dp.hip -- Davis-Putnam variable elimination (REF.py:98-130) on gfx950.
+//
+// One elimination step of the reference: pick `var = variables.pop()`, split
+// the clause list into clauses with var / with -var / without it, resolve
+// every (pos, neg) pair in list order, drop tautologies, return False on an
+// empty resolvent, keep a resolvent unless an earlier-listed clause of
+// `remaining + unique_new` is a subset of it, continue with remaining + kept.
+//
+// GPU formulation, per step (host C++ drives the launches, data stays in HBM):
+//   * every clause carries (a) a bitset key over the dense variable index for
+//     the set algebra (split, tautology, emptiness, subsumption) and (b) its
+//     CPython table image (pyset_dev.h), because the reference's elimination
+//     order is decided by CPython's set layout;
+//   * dp_firstpos: first-occurrence position of every variable in the order
+//     `{abs(lit) for clause in clauses for lit in clause}` visits them (list
+//     order, then each clause's table order); dp_pop: one workgroup ranks the
+//     variables by that position and replays the comprehension's insertions
+//     into a modelled set, then pops its first live slot;
+//   * dp_split + scans: order-preserving compaction into pos / neg / rem lists;
+//   * dp_diff: `pc - {var}` / `nc - {-var}` images, one thread per clause;
+//   * dp_pairs: one thread per pair, resolvent bitset, tautology / empty flags;
+//   * dp_subsume: greedy `unique_new` filter.  A new clause is dropped iff a
+//     remaining clause or an *earlier* new clause is a subset of it (an earlier
+//     new clause that was itself dropped was dropped for a subset that is also
+//     a subset of this one), so the greedy loop becomes one parallel test;
+//   * dp_build: `AX | BY` images of the kept resolvents; dp_assemble: the next
+//     clause list (rem in order, then kept in pair order).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "common.h"
+#include "prims.h"
+#include "pyset_dev.h"
+
+namespace satmi {
+
+// smallest power of two >= 8 that exceeds 8*u: room for every table a set of u
+// keys passes through (add: < 8u, merge: < 4u)
+static inline int64_t cap_for(int64_t u) {
+    int64_t c = PY_MINSIZE;
+    while (c <= 8 * u) c <<= 1;
+    return c;
+}
+
+struct ClauseList {   // device arrays of one generation
+    int64_t *off;      // table image offset in pool
+    int32_t *mask, *fill, *used;
+    uint64_t *bits;    // K words per clause
+    int32_t *pool;
+};
+
+__device__ __forceinline__ DView cl_view(const ClauseList &L, int64_t c) {
+    return {L.pool + L.off[c], (int64_t)L.mask[c], (int64_t)L.fill[c], (int64_t)L.used[c]};
+}
+
+// clauses = [set(clause) for clause in formula]  (REF.py:99); image c at pool + 2*cap*c
+__global__ void dp_encode_kernel(int nclauses, const int32_t *off, const int32_t *lits, const int32_t *var2dense,
+                                 int W, int64_t cap, ClauseList L, int *overflow) {
+    const int K = 2 * W;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nclauses; c += gridDim.x * blockDim.x) {
+        int32_t *a = L.pool + (int64_t)c * 2 * cap;
+        DSet s;
+        dset_init(s, a, a + cap, cap);
+        uint64_t *k = L.bits + (int64_t)c * K;
+        for (int w = 0; w < K; ++w) k[w] = 0ull;
+        for (int j = off[c]; j < off[c + 1]; ++j) {
+            const int x = lits[j];
+            py_add(s, x);
+            const int d = var2dense[x < 0 ? -x : x];
+            k[(x < 0 ? W : 0) + (d >> 6)] |= 1ull << (d & 63);
+        }
+        if (s.overflow) *overflow = 1;
+        L.off[c] = s.t - L.pool;
+        L.mask[c] = (int32_t)s.mask;
+        L.fill[c] = (int32_t)s.fill;
+        L.used[c] = (int32_t)s.used;
+    }
+}
+
+__global__ void dp_used_kernel(ClauseList L, int64_t n, int64_t *used) {
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
+        used[c] = L.used[c];
+}
+
+// first position of every variable in the comprehension's visiting order
+__global__ void dp_firstpos_kernel(ClauseList L, int64_t n, const int64_t *base, const int32_t *var2dense,
+                                   unsigned long long *firstpos) {
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
+        const DView s = cl_view(L, c);
+        int64_t p = base[c];
+        for (int64_t i = 0; i <= s.mask; ++i) {
+            const int32_t k = s.t[i];
+            if (k == PY_EMPTY || k == PY_DUMMY) continue;
+            atomicMin(&firstpos[var2dense[k < 0 ? -k : k]], (unsigned long long)p);
+            ++p;
+        }
+    }
+}
+
+// variables.pop() (REF.py:100-103, :128): one workgroup.  out[0] = popped
+// variable (0: the set is empty), out[1] = number of distinct variables.
+__global__ void __launch_bounds__(256) dp_pop_kernel(const unsigned long long *firstpos, const int32_t *dense2var,
+                                                     int V, int32_t *order, int32_t *scratch, int64_t cap,
+                                                     int32_t *out) {
+    __shared__ int nlive;
+    if (threadIdx.x == 0) nlive = 0;
+    __syncthreads();
+    for (int d = threadIdx.x; d < V; d += blockDim.x) {
+        const unsigned long long f = firstpos[d];
+        if (f == ~0ull) continue;
+        int rank = 0;
+        for (int e = 0; e < V; ++e) rank += firstpos[e] < f ? 1 : 0;   // positions are distinct
+        order[rank] = dense2var[d];
+        atomicAdd(&nlive, 1);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const int nv = nlive;
+    int32_t popped = 0;
+    if (nv > 0) {
+        DSet s;
+        dset_init(s, scratch, scratch + cap, cap);
+        for (int r = 0; r < nv; ++r) py_add(s, order[r]);
+        if (s.overflow) {
+            out[2] = 1;
+        } else {
+            for (int64_t i = 0; i <= s.mask; ++i)   // a fresh set's finger is 0: first live slot
+                if (s.t[i] != PY_EMPTY && s.t[i] != PY_DUMMY) {
+                    popped = s.t[i];
+                    break;
+                }
+        }
+    }
+    out[0] = popped;
+    out[1] = nv;
+}
+
+// split flags (REF.py:106-108)
+__global__ void dp_split_kernel(ClauseList L, int64_t n, int W, int d, int64_t *fpos, int64_t *fneg, int64_t *frem) {
+    const int K = 2 * W;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t *k = L.bits + c * K;
+        const bool p = (k[d >> 6] >> (d & 63)) & 1ull;
+        const bool q = (k[W + (d >> 6)] >> (d & 63)) & 1ull;
+        fpos[c] = p;
+        fneg[c] = q;
+        frem[c] = !p && !q;
+    }
+}
+
+__global__ void dp_compact_kernel(const int64_t *flag, const int64_t *pos, int64_t n, int64_t *out) {
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
+        if (flag[c]) out[pos[c]] = c;
+}
+
+__global__ void dp_maxused_kernel(ClauseList L, const int64_t *idx, int64_t n, unsigned long long *mx) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+        atomicMax(mx, (unsigned long long)L.used[idx[t]]);
+}
+
+struct Images {   // per-entry images built into 2*cap slots each
+    int32_t *pool;
+    int64_t *off;
+    int32_t *mask, *fill, *used;
+    int64_t cap;
+};
+
+__device__ __forceinline__ DView img_view(const Images &I, int64_t e) {
+    return {I.pool + I.off[e], (int64_t)I.mask[e], (int64_t)I.fill[e], (int64_t)I.used[e]};
+}
+
+// AX = pc - {var} for the pos list, BY = nc - {-var} for the neg list
+__global__ void dp_diff_kernel(ClauseList L, const int64_t *list, int64_t n, int32_t key, Images I, int *overflow) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        int32_t *a = I.pool + e * 2 * I.cap;
+        DSet s;
+        dset_init(s, a, a + I.cap, I.cap);
+        py_difference1(s, cl_view(L, list[e]), key);
+        if (s.overflow) *overflow = 1;
+        I.off[e] = s.t - I.pool;
+        I.mask[e] = (int32_t)s.mask;
+        I.fill[e] = (int32_t)s.fill;
+        I.used[e] = (int32_t)s.used;
+    }
+}
+
+// pair p = i*nn + j: resolvent bitset, tautology (REF.py:115) and empty (REF.py:117) flags
+__global__ void dp_pairs_kernel(ClauseList L, const int64_t *plist, const int64_t *nlist, int64_t nn, int64_t npairs,
+                                int W, int d, uint64_t *rbits, int64_t *nontaut, unsigned long long *first_empty) {
+    const int K = 2 * W;
+    const uint64_t vb = 1ull << (d & 63);
+    const int vw = d >> 6;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npairs;
+         p += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t *a = L.bits + plist[p / nn] * K, *b = L.bits + nlist[p % nn] * K;
+        uint64_t *r = rbits + p * K;
+        bool taut = false, empty = true;
+        for (int w = 0; w < W; ++w) {
+            // (pc - {var}) | (nc - {-var}): var leaves pc's positive half and
+            // -var nc's negative half only (a tautological pc keeps its -var)
+            const uint64_t keep = w == vw ? ~vb : ~0ull;
+            const uint64_t rp = (a[w] & keep) | b[w], rn = a[W + w] | (b[W + w] & keep);
+            r[w] = rp;
+            r[W + w] = rn;
+            taut |= (rp & rn) != 0ull;
+            empty &= (rp | rn) == 0ull;
+        }
+        nontaut[p] = !taut;
+        if (empty) atomicMin(first_empty, (unsigned long long)p);
+    }
+}
+
+__device__ __forceinline__ bool bits_subset(const uint64_t *a, const uint64_t *b, int K) {
+    for (int w = 0; w < K; ++w)
+        if (a[w] & ~b[w]) return false;
+    return true;
+}
+
+// unique_new (REF.py:122-125): kept[k] iff no rem clause and no earlier new clause is a subset
+__global__ void dp_subsume_kernel(ClauseList L, const int64_t *rlist, int64_t nrem, const uint64_t *rbits,
+                                  const int64_t *ntlist, int64_t m, int K, int64_t *kept) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t *x = rbits + ntlist[k] * K;
+        bool sub = false;
+        for (int64_t e = 0; e < nrem && !sub; ++e) sub = bits_subset(L.bits + rlist[e] * K, x, K);
+        for (int64_t e = 0; e < k && !sub; ++e) sub = bits_subset(rbits + ntlist[e] * K, x, K);
+        kept[k] = !sub;
+    }
+}
+
+// kept resolvent images: (pc - {var}) | (nc - {-var})  (REF.py:114)
+__global__ void dp_build_kernel(Images A, Images B, const int64_t *ntlist, const int64_t *kflag, const int64_t *kpos,
+                                int64_t m, int64_t nn, Images R, int *overflow) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        if (!kflag[k]) continue;
+        const int64_t p = ntlist[k], e = kpos[k];
+        int32_t *a = R.pool + e * 2 * R.cap;
+        DSet s;
+        dset_init(s, a, a + R.cap, R.cap);
+        py_merge(s, img_view(A, p / nn));   // set_copy(AX)
+        py_merge(s, img_view(B, p % nn));   // |= BY
+        if (s.overflow) *overflow = 1;
+        R.off[e] = s.t - R.pool;
+        R.mask[e] = (int32_t)s.mask;
+        R.fill[e] = (int32_t)s.fill;
+        R.used[e] = (int32_t)s.used;
+    }
+}
+
+__global__ void dp_sizes_kernel(ClauseList L, const int64_t *rlist, int64_t nrem, Images R, int64_t nkept,
+                                int64_t *size) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nrem + nkept;
+         t += (int64_t)gridDim.x * blockDim.x)
+        size[t] = (t < nrem ? L.mask[rlist[t]] : R.mask[t - nrem]) + 1;
+}
+
+// next generation: remaining_clauses + unique_new (REF.py:127)
+__global__ void dp_assemble_kernel(ClauseList L, const int64_t *rlist, int64_t nrem, Images R, const int64_t *klist,
+                                   int64_t nkept, const uint64_t *rbits, const int64_t *ntlist, const int64_t *off,
+                                   int K, ClauseList O) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nrem + nkept;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t *src;
+        const uint64_t *bsrc;
+        int32_t mask, fill, used;
+        if (t < nrem) {
+            const int64_t c = rlist[t];
+            src = L.pool + L.off[c];
+            bsrc = L.bits + c * K;
+            mask = L.mask[c];
+            fill = L.fill[c];
+            used = L.used[c];
+        } else {
+            const int64_t e = t - nrem;
+            src = R.pool + R.off[e];
+            bsrc = rbits + ntlist[klist[e]] * K;
+            mask = R.mask[e];
+            fill = R.fill[e];
+            used = R.used[e];
+        }
+        int32_t *dst = O.pool + off[t];
+        for (int32_t i = 0; i <= mask; ++i) dst[i] = src[i];
+        for (int w = 0; w < K; ++w) O.bits[t * K + w] = bsrc[w];
+        O.off[t] = off[t];
+        O.mask[t] = mask;
+        O.fill[t] = fill;
+        O.used[t] = used;
+    }
+}
+
+// ------------------------------------------------------------------ host side
+namespace {
+
+struct Buf {
+    void *p = nullptr;
+    size_t cap = 0;
+    ~Buf() {
+        if (p) (void)hipFree(p);
+    }
+    Buf() = default;
+    Buf(const Buf &) = delete;
+    int need(size_t bytes) {
+        if (bytes <= cap) return SATMI_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 2, 256);
+        SATMI_HIP(hipMalloc(&p, want));
+        cap = want;
+        return SATMI_OK;
+    }
+    template <class T>
+    T *as() const { return (T *)p; }
+};
+
+#define DP_TRY(x)                        \
+    do {                                 \
+        int _rc = (x);                   \
+        if (_rc != SATMI_OK) return _rc; \
+    } while (0)
+
+struct Gen {   // one generation of the clause list
+    Buf off, mask, fill, used, bits, pool;
+    int reserve(int64_t n, int K, int64_t pool_slots) {
+        DP_TRY(off.need(8 * (size_t)std::max<int64_t>(n, 1)));
+        DP_TRY(mask.need(4 * (size_t)std::max<int64_t>(n, 1)));
+        DP_TRY(fill.need(4 * (size_t)std::max<int64_t>(n, 1)));
+        DP_TRY(used.need(4 * (size_t)std::max<int64_t>(n, 1)));
+        DP_TRY(bits.need(8 * (size_t)std::max<int64_t>(n, 1) * K));
+        DP_TRY(pool.need(4 * (size_t)std::max<int64_t>(pool_slots, 1)));
+        return SATMI_OK;
+    }
+    ClauseList view() const {
+        return {off.as<int64_t>(), mask.as<int32_t>(), fill.as<int32_t>(), used.as<int32_t>(), bits.as<uint64_t>(),
+                pool.as<int32_t>()};
+    }
+};
+
+struct Img {
+    Buf pool, off, mask, fill, used;
+    int64_t cap = 8;
+    int reserve(int64_t n, int64_t c) {
+        cap = c;
+        n = std::max<int64_t>(n, 1);
+        DP_TRY(pool.need(4 * (size_t)n * 2 * c));
+        DP_TRY(off.need(8 * (size_t)n));
+        DP_TRY(mask.need(4 * (size_t)n));
+        DP_TRY(fill.need(4 * (size_t)n));
+        DP_TRY(used.need(4 * (size_t)n));
+        return SATMI_OK;
+    }
+    Images view() const {
+        return {pool.as<int32_t>(), off.as<int64_t>(), mask.as<int32_t>(), fill.as<int32_t>(), used.as<int32_t>(),
+                cap};
+    }
+};
+
+// ordered compaction of flag[n] into out (indices); returns the count
+int compact(const int64_t *flag, int64_t n, Buf &pos, Buf &tiles, Buf &grand, Buf &out, int64_t *count,
+            hipStream_t s) {
+    *count = 0;
+    if (n == 0) return SATMI_OK;
+    DP_TRY(pos.need(8 * (size_t)n));
+    DP_TRY(tiles.need(8 * (size_t)((n + SCAN_TILE - 1) / SCAN_TILE + 1)));
+    DP_TRY(grand.need(8));
+    DP_TRY(exclusive_scan(flag, pos.as<int64_t>(), n, tiles.as<int64_t>(), grand.as<int64_t>(), s));
+    SATMI_HIP(hipMemcpyAsync(count, grand.p, 8, hipMemcpyDeviceToHost, s));
+    SATMI_HIP(hipStreamSynchronize(s));
+    DP_TRY(out.need(8 * (size_t)std::max<int64_t>(*count, 1)));
+    hipLaunchKernelGGL(dp_compact_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, flag, pos.as<int64_t>(), n,
+                       out.as<int64_t>());
+    SATMI_HIP(hipGetLastError());
+    return SATMI_OK;
+}
+
+}  // namespace
+}  // namespace satmi
+
+using namespace satmi;
+
+extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_lits, int64_t step_limit,
+                             int64_t clause_limit, double time_limit_s, int32_t *h_result, int32_t *h_trace_vars,
+                             int trace_cap, int32_t *h_steps, int32_t *h_rec_lits, int64_t rec_lit_cap,
+                             int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_step_off,
+                             int rec_step_cap) {
+    if (nclauses < 0 || (nclauses > 0 && (!h_clause_off || !h_lits)) || !h_result || !h_steps) {
+        set_error("satmi_dp_host: bad arguments");
+        return SATMI_ERR_ARG;
+    }
+    const auto t_start = std::chrono::steady_clock::now();
+    *h_result = -1;
+    *h_steps = 0;
+    if (h_rec_step_off && rec_step_cap > 0) h_rec_step_off[0] = 0;
+    if (h_rec_clause_off && rec_clause_cap > 0) h_rec_clause_off[0] = 0;
+    const int64_t Ltot = nclauses > 0 ? h_clause_off[nclauses] : 0;
+    int maxvar = 0, maxlen = 0;
+    for (int c = 0; c < nclauses; ++c) maxlen = std::max(maxlen, h_clause_off[c + 1] - h_clause_off[c]);
+    for (int64_t i = 0; i < Ltot; ++i) {
+        if (h_lits[i] == 0 || h_lits[i] == INT32_MIN) {
+            set_error("satmi_dp_host: literal 0 / INT32_MIN");
+            return SATMI_ERR_ARG;
+        }
+        maxvar = std::max(maxvar, std::abs(h_lits[i]));
+    }
+    std::vector<int32_t> var2dense(maxvar + 1, -1), dense2var;
+    for (int64_t i = 0; i < Ltot; ++i) var2dense[std::abs(h_lits[i])] = 1;
+    for (int v = 1; v <= maxvar; ++v)
+        if (var2dense[v] >= 0) {
+            var2dense[v] = (int32_t)dense2var.size();
+            dense2var.push_back(v);
+        }
+    const int V = (int)dense2var.size();
+    const int W = std::max(1, (V + 63) / 64);
+    const int K = 2 * W;
+    hipStream_t s = nullptr;
+
+    Buf d_off, d_lits, d_v2d, d_d2v, flags, misc, firstpos, order, popscratch, base, usedtmp;
+    Buf fpos, fneg, frem, plist, nlist, rlist, scanpos, tiles, grand, rbits, nontaut, ntlist, kept, klist, kpos,
+        sizes, offs;
+    Gen g[2];
+    Img A, B, R;
+    DP_TRY(d_off.need(4 * (size_t)(nclauses + 1)));
+    DP_TRY(d_lits.need(4 * (size_t)std::max<int64_t>(Ltot, 1)));
+    DP_TRY(d_v2d.need(4 * (size_t)(maxvar + 1)));
+    DP_TRY(d_d2v.need(4 * (size_t)std::max(V, 1)));
+    DP_TRY(misc.need(64));
+    int cur = 0;
+    int64_t ncl = nclauses;
+    {
+        const int64_t cap0 = cap_for(maxlen);
+        DP_TRY(g[0].reserve(ncl, K, ncl * 2 * cap0));
+        if (nclauses > 0) {
+            SATMI_HIP(hipMemcpyAsync(d_off.p, h_clause_off, 4 * (size_t)(nclauses + 1), hipMemcpyHostToDevice, s));
+            if (Ltot) SATMI_HIP(hipMemcpyAsync(d_lits.p, h_lits, 4 * (size_t)Ltot, hipMemcpyHostToDevice, s));
+            SATMI_HIP(hipMemcpyAsync(d_v2d.p, var2dense.data(), 4 * (size_t)(maxvar + 1), hipMemcpyHostToDevice, s));
+        }
+        if (V) SATMI_HIP(hipMemcpyAsync(d_d2v.p, dense2var.data(), 4 * (size_t)V, hipMemcpyHostToDevice, s));
+        SATMI_HIP(hipMemsetAsync(misc.p, 0, 64, s));
+        if (nclauses > 0) {
+            hipLaunchKernelGGL(dp_encode_kernel, dim3(grid_for(nclauses)), dim3(PRIM_BLOCK), 0, s, nclauses,
+                               d_off.as<int32_t>(), d_lits.as<int32_t>(), d_v2d.as<int32_t>(), W, cap0,
+                               g[0].view(), misc.as<int>());
+            SATMI_HIP(hipGetLastError());
+        }
+    }
+    DP_TRY(firstpos.need(8 * (size_t)std::max(V, 1)));
+    DP_TRY(order.need(4 * (size_t)std::max(V, 1)));
+    const int64_t popcap = cap_for(V);
+    DP_TRY(popscratch.need(4 * (size_t)2 * popcap));
+    int steps = 0, result = 1;
+    int64_t rec_clauses = 0, rec_lits = 0;
+    std::vector<int32_t> h_pool;
+    std::vector<int64_t> h_off;
+    std::vector<int32_t> h_mask;
+    for (;;) {
+        // variables = {abs(lit) ...}; while variables: var = variables.pop()
+        if (ncl == 0) break;   // no clauses, no variables: True
+        ClauseList Lc = g[cur].view();
+        DP_TRY(base.need(8 * (size_t)ncl));
+        DP_TRY(usedtmp.need(8 * (size_t)ncl));
+        DP_TRY(tiles.need(8 * (size_t)((ncl + SCAN_TILE - 1) / SCAN_TILE + 1)));
+        DP_TRY(grand.need(8));
+        hipLaunchKernelGGL(dp_used_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, Lc, ncl,
+                           usedtmp.as<int64_t>());
+        DP_TRY(exclusive_scan(usedtmp.as<int64_t>(), base.as<int64_t>(), ncl, tiles.as<int64_t>(),
+                              grand.as<int64_t>(), s));
+        SATMI_HIP(hipMemsetAsync(firstpos.p, 0xff, 8 * (size_t)std::max(V, 1), s));
+        hipLaunchKernelGGL(dp_firstpos_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, Lc, ncl,
+                           base.as<int64_t>(), d_v2d.as<int32_t>(), firstpos.as<unsigned long long>());
+        hipLaunchKernelGGL(dp_pop_kernel, dim3(1), dim3(256), 0, s, firstpos.as<unsigned long long>(),
+                           d_d2v.as<int32_t>(), V, order.as<int32_t>(), popscratch.as<int32_t>(), popcap,
+                           misc.as<int32_t>() + 4);
+        SATMI_HIP(hipGetLastError());
+        int32_t pop[3] = {0, 0, 0};
+        int32_t ovf = 0;
+        SATMI_HIP(hipMemcpyAsync(pop, misc.as<int32_t>() + 4, 12, hipMemcpyDeviceToHost, s));
+        SATMI_HIP(hipMemcpyAsync(&ovf, misc.p, 4, hipMemcpyDeviceToHost, s));
+        SATMI_HIP(hipStreamSynchronize(s));
+        if (ovf || pop[2]) {
+            set_error("satmi_dp_host: set model table overflow");
+            return SATMI_ERR_TOO_LARGE;
+        }
+        if (pop[1] == 0) break;   // `while variables` ends: True (REF.py:130)
+        if (step_limit > 0 && steps >= step_limit) {
+            result = -1;
+            break;
+        }
+        if (time_limit_s > 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > time_limit_s) {
+            result = -1;
+            break;
+        }
+        const int32_t var = pop[0];
+        const int d = var2dense[var];
+        if (h_trace_vars && steps < trace_cap) h_trace_vars[steps] = var;
+        ++steps;
+        // split (REF.py:106-108)
+        DP_TRY(fpos.need(8 * (size_t)ncl));
+        DP_TRY(fneg.need(8 * (size_t)ncl));
+        DP_TRY(frem.need(8 * (size_t)ncl));
+        hipLaunchKernelGGL(dp_split_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, Lc, ncl, W, d,
+                           fpos.as<int64_t>(), fneg.as<int64_t>(), frem.as<int64_t>());
+        int64_t np = 0, nn = 0, nr = 0;
+        DP_TRY(compact(fpos.as<int64_t>(), ncl, scanpos, tiles, grand, plist, &np, s));
+        DP_TRY(compact(fneg.as<int64_t>(), ncl, scanpos, tiles, grand, nlist, &nn, s));
+        DP_TRY(compact(frem.as<int64_t>(), ncl, scanpos, tiles, grand, rlist, &nr, s));
+        const int64_t npairs = np * nn;
+        // resolvent bitsets + flags (REF.py:111-119)
+        int64_t m = 0;
+        unsigned long long first_empty = ~0ull;
+        if (npairs > 0) {
+            DP_TRY(rbits.need(8 * (size_t)npairs * K));
+            DP_TRY(nontaut.need(8 * (size_t)npairs));
+            SATMI_HIP(hipMemsetAsync(misc.as<char>() + 32, 0xff, 8, s));
+            hipLaunchKernelGGL(dp_pairs_kernel, dim3(grid_for(npairs)), dim3(PRIM_BLOCK), 0, s, Lc,
+                               plist.as<int64_t>(), nlist.as<int64_t>(), nn, npairs, W, d, rbits.as<uint64_t>(),
+                               nontaut.as<int64_t>(), (unsigned long long *)(misc.as<char>() + 32));
+            SATMI_HIP(hipGetLastError());
+            SATMI_HIP(hipMemcpyAsync(&first_empty, misc.as<char>() + 32, 8, hipMemcpyDeviceToHost, s));
+            DP_TRY(compact(nontaut.as<int64_t>(), npairs, scanpos, tiles, grand, ntlist, &m, s));
+        }
+        // the reference stops at the first empty resolvent, or (clause_limit) when
+        // remaining + new grows past the limit, whichever comes first in pair order
+        int64_t limit_pair = -1;
+        const int64_t kth = std::max<int64_t>(clause_limit - nr, 0);   // 0-based index of the offending new clause
+        if (clause_limit > 0 && m > kth) {
+            int64_t p = 0;
+            SATMI_HIP(hipMemcpyAsync(&p, ntlist.as<int64_t>() + kth, 8, hipMemcpyDeviceToHost, s));
+            SATMI_HIP(hipStreamSynchronize(s));
+            limit_pair = p;
+        }
+        if (first_empty != ~0ull && (limit_pair < 0 || (int64_t)first_empty <= limit_pair)) {
+            result = 0;   // empty clause: unsatisfiable (REF.py:117-118)
+            break;
+        }
+        if (limit_pair >= 0) {
+            result = -1;
+            break;
+        }
+        // unique_new (REF.py:122-125)
+        int64_t nkept = 0;
+        if (m > 0) {
+            DP_TRY(kept.need(8 * (size_t)m));
+            hipLaunchKernelGGL(dp_subsume_kernel, dim3(grid_for(m)), dim3(PRIM_BLOCK), 0, s, Lc,
+                               rlist.as<int64_t>(), nr, rbits.as<uint64_t>(), ntlist.as<int64_t>(), m, K,
+                               kept.as<int64_t>());
+            SATMI_HIP(hipGetLastError());
+            DP_TRY(compact(kept.as<int64_t>(), m, kpos, tiles, grand, klist, &nkept, s));
+        }
+        if (nkept > 0) {
+            // images of AX, BY and the kept resolvents
+            unsigned long long mx[2] = {0, 0};
+            SATMI_HIP(hipMemsetAsync(misc.as<char>() + 48, 0, 16, s));
+            hipLaunchKernelGGL(dp_maxused_kernel, dim3(grid_for(np)), dim3(PRIM_BLOCK), 0, s, Lc, plist.as<int64_t>(),
+                               np, (unsigned long long *)(misc.as<char>() + 48));
+            hipLaunchKernelGGL(dp_maxused_kernel, dim3(grid_for(nn)), dim3(PRIM_BLOCK), 0, s, Lc, nlist.as<int64_t>(),
+                               nn, (unsigned long long *)(misc.as<char>() + 56));
+            SATMI_HIP(hipMemcpyAsync(mx, misc.as<char>() + 48, 16, hipMemcpyDeviceToHost, s));
+            SATMI_HIP(hipStreamSynchronize(s));
+            DP_TRY(A.reserve(np, cap_for((int64_t)mx[0])));
+            DP_TRY(B.reserve(nn, cap_for((int64_t)mx[1])));
+            DP_TRY(R.reserve(nkept, cap_for((int64_t)mx[0] + (int64_t)mx[1])));
+            hipLaunchKernelGGL(dp_diff_kernel, dim3(grid_for(np)), dim3(PRIM_BLOCK), 0, s, Lc, plist.as<int64_t>(),
+                               np, var, A.view(), misc.as<int>());
+            hipLaunchKernelGGL(dp_diff_kernel, dim3(grid_for(nn)), dim3(PRIM_BLOCK), 0, s, Lc, nlist.as<int64_t>(),
+                               nn, -var, B.view(), misc.as<int>());
+            hipLaunchKernelGGL(dp_build_kernel, dim3(grid_for(m)), dim3(PRIM_BLOCK), 0, s, A.view(), B.view(),
+                               ntlist.as<int64_t>(), kept.as<int64_t>(), kpos.as<int64_t>(), m, nn, R.view(),
+                               misc.as<int>());
+            SATMI_HIP(hipGetLastError());
+        }
+        // clauses = remaining_clauses + unique_new (REF.py:127)
+        const int64_t ncl2 = nr + nkept;
+        int64_t pool2 = 0;
+        if (ncl2 > 0) {
+            DP_TRY(sizes.need(8 * (size_t)ncl2));
+            DP_TRY(offs.need(8 * (size_t)ncl2));
+            hipLaunchKernelGGL(dp_sizes_kernel, dim3(grid_for(ncl2)), dim3(PRIM_BLOCK), 0, s, Lc, rlist.as<int64_t>(),
+                               nr, R.view(), nkept, sizes.as<int64_t>());
+            DP_TRY(tiles.need(8 * (size_t)((ncl2 + SCAN_TILE - 1) / SCAN_TILE + 1)));
+            DP_TRY(exclusive_scan(sizes.as<int64_t>(), offs.as<int64_t>(), ncl2, tiles.as<int64_t>(),
+                                  grand.as<int64_t>(), s));
+            SATMI_HIP(hipMemcpyAsync(&pool2, grand.p, 8, hipMemcpyDeviceToHost, s));
+            SATMI_HIP(hipStreamSynchronize(s));
+            const int nxt = cur ^ 1;
+            DP_TRY(g[nxt].reserve(ncl2, K, pool2));
+            hipLaunchKernelGGL(dp_assemble_kernel, dim3(grid_for(ncl2)), dim3(PRIM_BLOCK), 0, s, Lc,
+                               rlist.as<int64_t>(), nr, R.view(), klist.as<int64_t>(), nkept, rbits.as<uint64_t>(),
+                               ntlist.as<int64_t>(), offs.as<int64_t>(), K, g[nxt].view());
+            SATMI_HIP(hipGetLastError());
+            cur = nxt;
+        }
+        ncl = ncl2;
+        // record the clause list after the step, each clause in its set iteration order
+        if (h_rec_lits && h_rec_clause_off && h_rec_step_off && steps < rec_step_cap) {
+            h_off.resize((size_t)std::max<int64_t>(ncl, 1));
+            h_mask.resize((size_t)std::max<int64_t>(ncl, 1));
+            h_pool.resize((size_t)std::max<int64_t>(pool2, 1));
+            if (ncl > 0) {
+                SATMI_HIP(hipMemcpyAsync(h_off.data(), g[cur].off.p, 8 * (size_t)ncl, hipMemcpyDeviceToHost, s));
+                SATMI_HIP(hipMemcpyAsync(h_mask.data(), g[cur].mask.p, 4 * (size_t)ncl, hipMemcpyDeviceToHost, s));
+                SATMI_HIP(hipMemcpyAsync(h_pool.data(), g[cur].pool.p, 4 * (size_t)pool2, hipMemcpyDeviceToHost, s));
+                SATMI_HIP(hipStreamSynchronize(s));
+            }
+            for (int64_t c = 0; c < ncl && rec_clauses + 1 < rec_clause_cap; ++c) {
+                for (int64_t i = 0; i <= h_mask[c]; ++i) {
+                    const int32_t k = h_pool[h_off[c] + i];
+                    if (k != PY_EMPTY && k != PY_DUMMY && rec_lits < rec_lit_cap) h_rec_lits[rec_lits++] = k;
+                }
+                h_rec_clause_off[++rec_clauses] = rec_lits;
+            }
+            h_rec_step_off[steps] = rec_clauses;
+        }
+        int32_t ovf2 = 0;
+        SATMI_HIP(hipMemcpyAsync(&ovf2, misc.p, 4, hipMemcpyDeviceToHost, s));
+        SATMI_HIP(hipStreamSynchronize(s));
+        if (ovf2) {
+            set_error("satmi_dp_host: set model table overflow");
+            return SATMI_ERR_TOO_LARGE;
+        }
+    }
+    SATMI_HIP(hipStreamSynchronize(s));
+    *h_result = result;
+    *h_steps = steps;
+    return SATMI_OK;
+}

@@ -1,0 +1,217 @@
+// pyset_dev.h -- device model of CPython 3.10 `set` tables for int keys.
+//
+// davis_putnam_solver (REF.py:98-130) chooses the variable to eliminate with
+// `variables.pop()` on `{abs(lit) for clause in clauses for lit in clause}`.
+// Which variable that is depends on CPython's open-addressing layout of that
+// set, which depends on the order the clause sets iterate, which depends on
+// how each clause set was built: `set(list)` (REF.py:99), `pc - {var}`,
+// `nc - {-var}` and their union `|` (REF.py:114).  To eliminate variables in
+// the reference's order -- and so produce its intermediate clause lists -- a
+// clause carries its table image: slots of int32 keys (0 = empty, INT32_MIN =
+// dummy), mask, fill and used.  The operations below follow
+// Objects/setobject.c of CPython 3.10: set_add_entry (9 linear probes, then
+// perturbed probing), set_insert_clean, set_table_resize (new size = smallest
+// power of two above 4*used, dummies dropped), set_merge (its resize rule,
+// table-copy and insert-clean fast paths), set_difference (copy-and-discard
+// when len(a) >> 2 > len(b)), set_lookkey / set_discard_entry and set_pop.
+// int hash: hash(k) = k, except hash(-1) == -2.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace satmi {
+
+constexpr int32_t PY_EMPTY = 0;
+constexpr int32_t PY_DUMMY = INT32_MIN;
+constexpr int PY_MINSIZE = 8;
+constexpr int PY_LINEAR_PROBES = 9;
+constexpr int PY_PERTURB_SHIFT = 5;
+
+__host__ __device__ __forceinline__ int64_t py_hash(int32_t k) { return k == -1 ? -2 : (int64_t)k; }
+
+// A set under construction: table `t` of mask+1 slots, and a spare buffer of
+// the same capacity that a resize rebuilds into.  `cap` bounds both.
+struct DSet {
+    int32_t *t;
+    int32_t *spare;
+    int64_t mask, fill, used;
+    int64_t cap;
+    bool overflow;
+};
+
+// read-only view of a stored table image
+struct DView {
+    const int32_t *t;
+    int64_t mask, fill, used;
+};
+
+__device__ __forceinline__ void dset_init(DSet &s, int32_t *a, int32_t *b, int64_t cap) {
+    s.t = a;
+    s.spare = b;
+    s.cap = cap;
+    s.mask = PY_MINSIZE - 1;
+    s.fill = s.used = 0;
+    s.overflow = cap < PY_MINSIZE;
+    for (int i = 0; i < PY_MINSIZE && i < cap; ++i) a[i] = PY_EMPTY;
+}
+
+__device__ __forceinline__ DView dset_view(const DSet &s) { return {s.t, s.mask, s.fill, s.used}; }
+
+__device__ void py_insert_clean(int32_t *table, uint64_t mask, int32_t key) {
+    const int64_t h = py_hash(key);
+    uint64_t perturb = (uint64_t)h;
+    uint64_t i = (uint64_t)h & mask;
+    for (;;) {
+        if (table[i] == PY_EMPTY) {
+            table[i] = key;
+            return;
+        }
+        if (i + PY_LINEAR_PROBES <= mask) {
+            for (int j = 1; j <= PY_LINEAR_PROBES; ++j) {
+                if (table[i + j] == PY_EMPTY) {
+                    table[i + j] = key;
+                    return;
+                }
+            }
+        }
+        perturb >>= PY_PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+// set_table_resize(so, minused)
+__device__ void py_resize(DSet &s, int64_t minused) {
+    int64_t newsize = PY_MINSIZE;
+    while (newsize <= minused) newsize <<= 1;
+    if (newsize == PY_MINSIZE && s.mask == PY_MINSIZE - 1 && s.fill == s.used) return;   // small table, no dummies
+    if (newsize > s.cap) {
+        s.overflow = true;
+        return;
+    }
+    int32_t *nt = s.spare;
+    for (int64_t i = 0; i < newsize; ++i) nt[i] = PY_EMPTY;
+    for (int64_t i = 0; i <= s.mask; ++i) {
+        const int32_t k = s.t[i];
+        if (k != PY_EMPTY && k != PY_DUMMY) py_insert_clean(nt, (uint64_t)(newsize - 1), k);
+    }
+    s.spare = s.t;
+    s.t = nt;
+    s.mask = newsize - 1;
+    s.fill = s.used;
+}
+
+// set_add_entry(so, key, hash)
+__device__ void py_add(DSet &s, int32_t key) {
+    if (s.overflow) return;
+    const int64_t h = py_hash(key);
+    const uint64_t mask = (uint64_t)s.mask;
+    uint64_t i = (uint64_t)h & mask;
+    int64_t slot = (int64_t)i;
+    if (s.t[i] != PY_EMPTY) {
+        int64_t freeslot = -1;
+        uint64_t perturb = (uint64_t)h;
+        for (;;) {
+            int32_t k = s.t[i];
+            if (k == key) return;                               // found_active
+            if (k == PY_DUMMY) freeslot = (int64_t)i;
+            bool hit_empty = false;
+            if (i + PY_LINEAR_PROBES <= mask) {
+                for (int j = 1; j <= PY_LINEAR_PROBES; ++j) {
+                    k = s.t[i + j];
+                    if (k == PY_EMPTY) {
+                        slot = (int64_t)(i + j);
+                        hit_empty = true;
+                        break;
+                    }
+                    if (k == key) return;
+                    if (k == PY_DUMMY) freeslot = (int64_t)(i + j);
+                }
+            }
+            if (!hit_empty) {
+                perturb >>= PY_PERTURB_SHIFT;
+                i = (i * 5 + 1 + perturb) & mask;
+                if (s.t[i] != PY_EMPTY) continue;
+                slot = (int64_t)i;
+            }
+            // found_unused_or_dummy
+            if (freeslot >= 0) {
+                s.used++;
+                s.t[freeslot] = key;
+                return;
+            }
+            break;
+        }
+    }
+    // found_unused
+    s.fill++;
+    s.used++;
+    s.t[slot] = key;
+    if ((uint64_t)s.fill * 5 < mask * 3) return;
+    py_resize(s, s.used > 50000 ? s.used * 2 : s.used * 4);
+}
+
+// set_lookkey: slot of key or -1
+__device__ int64_t py_find(const DView &s, int32_t key) {
+    const int64_t h = py_hash(key);
+    const uint64_t mask = (uint64_t)s.mask;
+    uint64_t perturb = (uint64_t)h;
+    uint64_t i = (uint64_t)h & mask;
+    for (;;) {
+        const int probes = (i + PY_LINEAR_PROBES <= mask) ? PY_LINEAR_PROBES : 0;
+        for (int j = 0; j <= probes; ++j) {
+            const int32_t k = s.t[i + j];
+            if (k == PY_EMPTY) return -1;
+            if (k == key) return (int64_t)(i + j);
+        }
+        perturb >>= PY_PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+// set_merge(so, other)
+__device__ void py_merge(DSet &s, const DView &o) {
+    if (s.overflow || o.used == 0) return;
+    if ((s.fill + o.used) * 5 >= s.mask * 3) {
+        py_resize(s, (s.used + o.used) * 2);
+        if (s.overflow) return;
+    }
+    if (s.fill == 0 && s.mask == o.mask && o.fill == o.used) {   // empty target, same size, no dummies: copy
+        for (int64_t i = 0; i <= o.mask; ++i) s.t[i] = o.t[i];
+        s.fill = o.fill;
+        s.used = o.used;
+        return;
+    }
+    if (s.fill == 0) {   // empty target: insert_clean
+        s.fill = o.used;
+        s.used = o.used;
+        for (int64_t i = 0; i <= o.mask; ++i) {
+            const int32_t k = o.t[i];
+            if (k != PY_EMPTY && k != PY_DUMMY) py_insert_clean(s.t, (uint64_t)s.mask, k);
+        }
+        return;
+    }
+    for (int64_t i = 0; i <= o.mask; ++i) {
+        const int32_t k = o.t[i];
+        if (k != PY_EMPTY && k != PY_DUMMY) py_add(s, k);
+    }
+}
+
+// dst = a - {key}   (set_difference with a one-element right operand)
+__device__ void py_difference1(DSet &dst, const DView &a, int32_t key) {
+    if ((a.used >> 2) > 1) {   // set_copy_and_difference: copy, then discard -> dummy
+        py_merge(dst, a);
+        if (dst.overflow) return;
+        const int64_t at = py_find(dset_view(dst), key);
+        if (at >= 0) {
+            dst.t[at] = PY_DUMMY;
+            dst.used--;
+        }
+        return;
+    }
+    for (int64_t i = 0; i <= a.mask; ++i) {
+        const int32_t k = a.t[i];
+        if (k != PY_EMPTY && k != PY_DUMMY && k != key) py_add(dst, k);
+    }
+}
+
+}  // namespace satmi

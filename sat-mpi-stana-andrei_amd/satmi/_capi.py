@@ -26,6 +26,7 @@ EXPORTED = (
     "satmi_abi_version", "satmi_last_error", "satmi_device_count", "satmi_set_device", "satmi_synchronize",
     "satmi_malloc", "satmi_free", "satmi_memcpy_h2d", "satmi_memcpy_d2h", "satmi_stream_synchronize",
     "satmi_dpll_batch_device", "satmi_dpll_batch_host", "satmi_dpll_lds_bytes", "satmi_resolution_host",
+    "satmi_dp_host",
 )
 
 
@@ -75,6 +76,9 @@ def load():
     L.satmi_resolution_host.argtypes = [
         ctypes.c_int, i32p, i32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
         i32p, i32p, i64p, ctypes.c_int, i32p, ctypes.c_int64, i64p, ctypes.c_int64, i64p, ctypes.c_int]
+    L.satmi_dp_host.argtypes = [
+        ctypes.c_int, i32p, i32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, i32p, i32p, ctypes.c_int, i32p,
+        i32p, ctypes.c_int64, i64p, ctypes.c_int64, i64p, ctypes.c_int]
     for name in EXPORTED:
         getattr(L, name)  # AttributeError here = library/header mismatch
     _lib = L

@@ -1,0 +1,76 @@
+"""GPU parity of Davis-Putnam elimination (csrc/dp.hip) through the C ABI: the
+eliminated variables (CPython's set.pop() order, modelled on the device) and
+every intermediate clause list -- each clause in its Python set iteration
+order -- against the reference's own outputs (tests/golden/dp_ref.json) and
+the CPU oracle."""
+import json
+import os
+import random
+
+import pytest
+
+import oracle
+from satmi import cnf
+from satmi.dp import eliminate
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases(golden_dir):
+    with open(os.path.join(golden_dir, "dp_ref.json")) as fh:
+        return json.load(fh)["cases"]
+
+
+def test_matches_reference_golden(golden_dir):
+    for c in _cases(golden_dir):
+        r = eliminate(c["formula"], record=True, time_limit=60.0)
+        assert r["result"] == int(c["result"]), c["formula"]
+        assert r["vars"] == [s["var"] for s in c["steps"]], c["formula"]
+        for k, s in enumerate(c["steps"]):
+            if "clauses" in s:
+                assert r["clauses"][k] == s["clauses"], (c["formula"], k)
+
+
+def _completed(o):
+    return o["steps"] if o["result"] == 1 else max(o["steps"] - 1, 0)
+
+
+def test_matches_oracle_random():
+    rng = random.Random(29)
+    for it in range(120):
+        n = rng.randint(2, 12)
+        m = rng.randint(1, 30)
+        f = [[v if rng.random() < 0.5 else -v for v in rng.sample(range(1, n + 1), rng.randint(1, min(4, n)))]
+             for _ in range(m)]
+        if it % 9 == 0:
+            f.append([1, -1] + ([2] if n > 1 else []))      # tautological clause: in the pos and neg lists
+        if it % 5 == 0:
+            f.append(list(f[0]))                             # duplicate clause
+        if it % 4 == 1:
+            f = [[x * 37 for x in c] for c in f]             # sparse ids: collisions in the set tables
+        if it % 7 == 3:
+            f = [c + [c[0]] for c in f]                      # duplicate literals inside clauses
+        o = oracle.dp(f, record=True)
+        r = eliminate(f, record=True, time_limit=60.0)
+        assert r["result"] == o["result"], f
+        assert r["vars"] == o["vars"], f
+        assert r["clauses"] == o["clauses"][:_completed(o)], f
+
+
+def test_edge_cases_and_pigeonhole():
+    for f in ([], [[]], [[1]], [[1], [-1]], [[1, -1]], [[1, 1], [-1]], [[1, 2], [], [-1]],
+              cnf.pigeonhole(2), cnf.pigeonhole(3)):
+        o = oracle.dp(f, record=True)
+        r = eliminate(f, record=True)
+        assert (r["result"], r["vars"]) == (o["result"], o["vars"]), f
+        assert r["clauses"] == o["clauses"][:_completed(o)], f
+
+
+def test_limits():
+    f = cnf.uniform_ksat(1, 14, 60, 3, seed=9).instance(0)
+    o = oracle.dp(f, step_limit=2)
+    r = eliminate(f, step_limit=2)
+    assert (r["result"], r["vars"]) == (o["result"], o["vars"]) and r["result"] == -1
+    o = oracle.dp(f, clause_limit=70)
+    r = eliminate(f, clause_limit=70)
+    assert (r["result"], r["vars"]) == (o["result"], o["vars"])
