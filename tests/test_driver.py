@@ -1,0 +1,77 @@
+"""The comparison / report driver (satmi/driver.py) on CPU: the report format
+against a block of the reference's own rezultat.txt (tests/golden/
+rezultat_block.txt), result strings, the deadline mapping, and a scripted menu
+session on stub solvers (the real solvers need the GPU: tests/test_driver_gpu.py)."""
+import os
+
+import pytest
+
+from satmi import driver
+from satmi.solvers import SolverTimeout
+
+
+def _formula_50x10():
+    # 50 clauses over 10 variables with 305 literals: the statistics of the fixture block
+    return ([[(i + j) % 10 + 1 for j in range(6)] for i in range(45)] +
+            [[(i + j) % 10 + 1 for j in range(7)] for i in range(5)])
+
+
+def test_report_matches_reference_block(tmp_path, monkeypatch, golden_dir):
+    with open(os.path.join(golden_dir, "rezultat_block.txt")) as fh:
+        expected = fh.read()
+    monkeypatch.setattr(driver.time, "strftime", lambda fmt: "2025-05-10 14:54:22")
+    results = {
+        "Resolution": {"time": 60, "memory": 722.88, "output": "Timeout after 60 seconds"},
+        "Davis-Putnam": {"time": 0.109294, "memory": 31.44, "output": "Formula is satisfiable"},
+        "DPLL": {"time": 60, "memory": 31.12, "output": "Timeout after 60 seconds"},
+        "PySAT": {"time": 0.10798, "memory": 31.0,
+                  "output": "Found 1 solution(s)\nFirst assignment sample: {1: False, 2: True, 3: False}..."},
+        "Hybrid": {"time": 60, "memory": 31.02, "output": "Timeout after 60 seconds"},
+    }
+    out = tmp_path / "rezultat.txt"
+    driver.save_results_to_file(_formula_50x10(), results, str(out))
+    assert out.read_text() == expected
+
+
+def test_describe_result():
+    assert driver.describe_result("Resolution", False) == "Formula is unsatisfiable"
+    assert driver.describe_result("Davis-Putnam", True) == "Formula is satisfiable"
+    assert driver.describe_result("DPLL", []) == "No solutions found"
+    assert driver.describe_result("DPLL", [{1: True, 2: False}, {1: False}]) == \
+        "Found 2 solution(s)\nFirst assignment sample: {1: True, 2: False}..."
+    assert driver.describe_result("CDCL", (True, {3: True})) == "Formula is satisfiable\nAssignment sample: {3: True}..."
+
+
+def test_execute_with_timeout_maps_deadlines_and_errors():
+    def late(f):
+        raise SolverTimeout("deadline")
+
+    def broken(f):
+        raise ValueError("bad formula")
+
+    assert driver.execute_with_timeout(lambda f: len(f), [[1]], 60) == (1, None)
+    assert driver.execute_with_timeout(late, [[1]], 60) == (None, "Timeout after 60 seconds")
+    assert driver.execute_with_timeout(broken, [[1]], 60) == (None, "bad formula")
+
+
+def test_read_formula_from_input():
+    feed = iter(["1 -2 0", "3", "x", "0 1 0", "2 0", "done"])
+    printed = []
+    f = driver.read_formula_from_input(lambda prompt: next(feed), printed.append)
+    assert f == [[1, -2], [2]]
+    assert "Error: Clause must end with 0" in printed and "Error: Please enter integers only" in printed
+    assert "Error: 0 can only appear at end of clause" in printed
+
+
+def test_scripted_menu_session(tmp_path):
+    table = {"1": ("Resolution", lambda f: False), "3": ("DPLL", lambda f: [{1: True}]),
+             "4": ("CDCL", driver.cdcl_solve)}
+    feed = iter(["1", "1 0", "-1 0", "done", "7", "y", "2", "3"])
+    printed = []
+    report = tmp_path / "rezultat.txt"
+    driver.main_menu(lambda prompt: next(feed), printed.append, solver_table=table, report_file=str(report))
+    text = report.read_text()
+    assert "Resolution" in text and "Formula is unsatisfiable" in text
+    assert "Found 1 solution(s)" in text
+    assert "CDCL            Error        " in text   # unimplemented solver is reported as an error row
+    assert printed[-1] == "Exiting program."

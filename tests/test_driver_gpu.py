@@ -1,0 +1,30 @@
+"""The comparison driver end to end on the GPU solvers: a scripted menu session
+(REF.py:491-632) whose saved report carries the verdicts the reference's own
+solvers give for the same formula (the oracle restates them)."""
+import pytest
+
+import oracle
+from satmi import driver
+
+pytestmark = pytest.mark.gpu
+
+
+def test_menu_session_on_gpu_solvers(tmp_path):
+    formula_lines = ["1 2 0", "-1 2 0", "1 -2 0", "-1 -2 0", "3 -4 0"]
+    feed = iter(["1"] + formula_lines + ["done", "1,2,3,6", "y", "2", "3"])
+    printed = []
+    report = tmp_path / "rezultat.txt"
+    driver.main_menu(lambda prompt: next(feed), printed.append, report_file=str(report))
+    text = report.read_text()
+    f = [[int(x) for x in line.split()[:-1]] for line in formula_lines]
+    res = oracle.resolution(f)["result"]
+    dp = oracle.dp(f)["result"]
+    want_res = "Formula is " + ("satisfiable" if res == 1 else "unsatisfiable")
+    want_dp = "Formula is " + ("satisfiable" if dp == 1 else "unsatisfiable")
+    rows = {line[:15].strip(): line for line in text.splitlines() if line[:15].strip() in
+            ("Resolution", "Davis-Putnam", "DPLL", "Hybrid")}
+    assert want_res in rows["Resolution"] and want_dp in rows["Davis-Putnam"]
+    nsol = len(oracle.dpll(f, "ref")["solutions"])
+    want = f"Found {nsol} solution(s)" if nsol else "No solutions found"
+    assert want in rows["DPLL"] and want in rows["Hybrid"]
+    assert "- Clauses: 5" in text and "- Variables: 4" in text
