@@ -11,6 +11,15 @@ step's verdict/counter totals.  The batch is BASELINE.json configs[2]: 262,144
 instances of n=100, alpha=4.26 per step, sharded across the ranks with no
 data-path collective (strong scaling: 262,144 / N instances per GPU).
 
+--workload selects the other BASELINE.json configs (parity-test cases, measured
+with the same harness; the default line is configs[2]):
+    3sat-n50   configs[1]: 4,096 instances of n=50, alpha=4.26
+    uf250      configs[4]: uf250-1065 shape (random 3-SAT n=250, m=1065),
+               node-capped search (--node-limit, default 20,000 calls/instance)
+    5sat-n200  configs[4]: random 5-SAT n=200 at the 5-SAT threshold
+               (alpha=21.117, m=4,223): long clauses, 1 wave per CU of LDS
+For the node-capped workloads the headline value is unit-props/s.
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -30,7 +39,16 @@ from satmi.shard import shard_range  # noqa: E402
 
 METRIC = "instances solved/sec, random 3-SAT n=100 α=4.26; unit-props/sec; HBM GB/s"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-KERNEL = "dpll_batch_kernel"
+KERNELS = {_capi.KERNEL_SCAN: "dpll_scan_kernel", _capi.KERNEL_GENERAL: "dpll_batch_kernel"}
+
+
+# workload presets: (total instances per step, n, alpha, k, node_limit, BASELINE config)
+WORKLOADS = {
+    "3sat-n100": (262144, 100, 4.26, 3, 0, "configs[2]"),
+    "3sat-n50": (4096, 50, 4.26, 3, 0, "configs[1]"),
+    "uf250": (4096, 250, 4.26, 3, 20000, "configs[4]"),
+    "5sat-n200": (1024, 200, 21.117, 5, 20000, "configs[4]"),
+}
 
 
 def parse():
@@ -38,18 +56,27 @@ def parse():
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--total", type=int, default=262144, help="instances per step, all ranks (configs[2])")
-    p.add_argument("--n", type=int, default=100)
-    p.add_argument("--alpha", type=float, default=4.26)
-    p.add_argument("--k", type=int, default=3)
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="3sat-n100")
+    p.add_argument("--total", type=int, default=None, help="instances per step, all ranks")
+    p.add_argument("--n", type=int, default=None)
+    p.add_argument("--alpha", type=float, default=None)
+    p.add_argument("--k", type=int, default=None)
+    p.add_argument("--node-limit", type=int, default=None, help="dpll calls per instance (0 = none)")
     p.add_argument("--seed", type=int, default=20251016)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-steps", action="store_true", help="no warmup/cpu leg (for rocprofv3 runs)")
-    return p.parse_args()
+    a = p.parse_args()
+    total, n, alpha, k, node_limit, a.config_name = WORKLOADS[a.workload]
+    a.total = total if a.total is None else a.total
+    a.n = n if a.n is None else a.n
+    a.alpha = alpha if a.alpha is None else a.alpha
+    a.k = k if a.k is None else a.k
+    a.node_limit = node_limit if a.node_limit is None else a.node_limit
+    return a
 
 
-def cpu_baseline(batch_host, seconds):
+def cpu_baseline(batch_host, seconds, node_limit):
     """The CPU oracle (oracle/, a C restatement of REF.py's DPLL, SOUND mode) on
     rank 0's host: one core, instances of the same batch until `seconds` pass."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -59,16 +86,19 @@ def cpu_baseline(batch_host, seconds):
     done = 0
     props = 0
     while done < batch_host.num_instances:
-        r = oracle.dpll(batch_host.instance(done), "sound", max_solutions=1, sol_cap=1)
+        r = oracle.dpll(batch_host.instance(done), "sound", max_solutions=1, sol_cap=1, node_limit=node_limit)
         props += r["counters"]["unit_props"]
         done += 1
         if time.perf_counter() - t0 > seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "instances/s", "cores": 1, "kind": "port",
-            "sample": f"first {done} instances of the rank-0 bench batch (same n/alpha), "
+    capped = node_limit > 0
+    return {"value": props / dt if capped else done / dt, "unit": "unit-props/s" if capped else "instances/s",
+            "cores": 1, "kind": "port",
+            "sample": f"first {done} instances of the rank-0 bench batch (same n/alpha"
+                      f"{', node limit %d' % node_limit if capped else ''}), "
                       f"oracle/sat_oracle.c SOUND mode, single thread, {dt:.1f} s",
-            "unit_props_per_s": props / dt}
+            "instances_per_s": done / dt, "unit_props_per_s": props / dt}
 
 
 def load_pmc(workload_key):
@@ -108,8 +138,8 @@ def main():
     def launch(j):
         icb, clb, lits, nv = batches[j % 2]
         rc = L.satmi_dpll_batch_device(
-            B, icb.data_ptr(), clb.data_ptr(), lits.data_ptr(), nv.data_ptr(), n, m, m * k, None, None,
-            _capi.MODE_SOUND, 1, 0, 0.0, 1, n, status.data_ptr(), counters.data_ptr(), sol_len.data_ptr(),
+            B, icb.data_ptr(), clb.data_ptr(), lits.data_ptr(), nv.data_ptr(), n, m, m * k, k, None, None,
+            _capi.MODE_SOUND, 1, args.node_limit, 0.0, 1, n, status.data_ptr(), counters.data_ptr(), sol_len.data_ptr(),
             sol_lits.data_ptr(), None, None, stream.cuda_stream)
         _capi.check(rc, "satmi_dpll_batch_device")
 
@@ -120,7 +150,7 @@ def main():
         if evs is not None:
             evs[1].record(stream)
         agg = torch.stack([(counters[:, 5] > 0).sum(), counters[:, 2].sum(), counters[:, 0].sum(),
-                           (status > 1).sum(), (sol_len.to(torch.int64) * 4 + 4 * (counters[:, 5] > 0)).sum(),
+                           (status > 2).sum() + (status == 2).sum() * (args.node_limit == 0), (sol_len.to(torch.int64) * 4 + 4 * (counters[:, 5] > 0)).sum(),
                            counters[:, 7].sum(), torch.tensor(B, device=dev, dtype=torch.int64)])
         if world > 1:
             dist.all_reduce(agg)   # RCCL: gather verdict/counter totals
@@ -151,7 +181,9 @@ def main():
     kernel_ms = sum(kms) / len(kms)
     tot = totals.tolist()
     nsat, props, nodes, bad, written, ticks, all_inst = tot
-    value = all_inst / elapsed
+    capped = args.node_limit > 0
+    # node-capped workloads (configs[4]) measure search throughput: unit-props/s
+    value = props / elapsed if capped else all_inst / elapsed
 
     # correctness spot check outside the timed region: every reported model satisfies its formula
     icb, clb, lits, nv = batches[(args.steps - 1) % 2]
@@ -175,30 +207,34 @@ def main():
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     workload = f"dpll_sound_{k}sat_n{n}_a{args.alpha}_B{B}"
     # resident waves of the persistent grid -> how busy the waves were (tail of the batch)
-    lds = L.satmi_dpll_lds_bytes(n, m, m * k)
-    per_cu = 0
-    for wpg in (4, 2, 1):
-        wgs = min(16, (160 * 1024) // (lds * wpg))
-        if wgs >= 1:
-            per_cu = max(per_cu, min(32, wgs * wpg))
+    kern, lds, per_cu = _capi.plan(n, m, m * k, k)
     resident = min(B, torch.cuda.get_device_properties(dev).multi_processor_count * per_cu)
     util = ticks / world * 1e-8 / (resident * kernel_ms * 1e-3 * args.steps)
     pmc = load_pmc(workload)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-            "kernel": KERNEL, "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes}
+            "kernel": KERNELS[kern], "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes}
 
+    if capped:
+        desc = (f"node-capped batched DPLL (SOUND mode, <= {args.node_limit} calls per instance), random {k}-SAT "
+                f"n={n} alpha={args.alpha} m={m}, {args.total} instances per step sharded over {world} GPU(s) "
+                f"(BASELINE {args.config_name})")
+    else:
+        desc = (f"batched DPLL (SOUND mode, first model = SAT/UNSAT decision), random {k}-SAT "
+                f"n={n} alpha={args.alpha} m={m}, {args.total} instances per step sharded over "
+                f"{world} GPU(s) (BASELINE {args.config_name})")
     out = {
-        "metric": METRIC, "value": value, "unit": "instances/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC, "value": value, "unit": "unit-props/s" if capped else "instances/s", "n_gpus": world, "steps": args.steps,
         "warmup": warm, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int32",
         "data": "synthetic: uniform random k-SAT generated in HBM (seeded), 2 batches alternated",
-        "config": {"workload": f"batched DPLL (SOUND mode, first model = SAT/UNSAT decision), random {k}-SAT "
-                               f"n={n} alpha={args.alpha} m={m}, {args.total} instances per step sharded over "
-                               f"{world} GPU(s) (BASELINE configs[2])",
+        "config": {"workload": desc, "preset": args.workload, "node_limit": args.node_limit,
                    "instances_per_step": args.total, "instances_per_gpu": B, "n": n, "m": m, "k": k,
                    "parallelism": f"instance-sharded x{world}"},
+        "instances_per_s": all_inst / elapsed,
         "unit_props_per_s": props / elapsed,
+        "capped_fraction": int(((status == 2).sum()).item()) / B,
+        "lds_bytes_per_wave": int(lds), "resident_waves": int(resident),
         "nodes_per_s": nodes / elapsed,
         "sat_fraction": nsat / all_inst,
         "hbm_gbs": achieved,
@@ -208,7 +244,7 @@ def main():
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and not args.profile_steps:
             host = cnf.CnfBatch(icb.cpu().numpy(), clb.cpu().numpy(), lits.cpu().numpy(), nv.cpu().numpy())
-            out["cpu_baseline"] = cpu_baseline(host, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(host, args.cpu_seconds, args.node_limit)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SATMI_ABI_VERSION 1
+#define SATMI_ABI_VERSION 2
 
 /* return codes */
 #define SATMI_OK 0
@@ -77,6 +77,11 @@ int satmi_stream_synchronize(void *stream);
  *   node_limit     stop after this many dpll calls (0 = none)
  *   time_limit_s   per-instance wall-clock limit (<= 0 = none)
  *   max_vars/max_clauses/max_lits   maxima over the batch (size the LDS layout)
+ *   max_clause_len longest clause of the batch, with every clause non-empty;
+ *                  0 = unknown.  SOUND mode without a caller assignment and
+ *                  1 <= max_clause_len <= 5, max_vars <= 2047 runs the
+ *                  clause-scan kernel (same results; see satmi_dpll_set_kernel);
+ *                  an instance that breaks the promise gets SATMI_DPLL_TOO_LARGE
  *   d_init_begin/d_init_lits        optional caller assignment (REF.py:133's
  *                  `assignment`), as signed literals in dict order; may be NULL
  *   sol_cap        solutions stored per instance; sol_stride >= max assignment size
@@ -90,7 +95,7 @@ int satmi_stream_synchronize(void *stream);
 int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_clause_begin,
                             const int32_t *d_clause_lit_begin, const int32_t *d_lits,
                             const int32_t *d_inst_nvars, int max_vars, int max_clauses, int max_lits,
-                            const int32_t *d_init_begin, const int32_t *d_init_lits,
+                            int max_clause_len, const int32_t *d_init_begin, const int32_t *d_init_lits,
                             int mode, int64_t max_solutions, int64_t node_limit, double time_limit_s,
                             int sol_cap, int sol_stride,
                             int32_t *d_status, int64_t *d_counters, int32_t *d_sol_len,
@@ -146,6 +151,24 @@ int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_li
 
 /* LDS bytes one wavefront needs for an instance of this size (0 = unsupported). */
 uint64_t satmi_dpll_lds_bytes(int max_vars, int max_clauses, int max_lits);
+
+/* Same for the clause-scan kernel (0 = the shape is not eligible for it). */
+uint64_t satmi_dpll_scan_lds_bytes(int max_vars, int max_clauses, int max_lits, int max_clause_len);
+
+/* Which DPLL kernel satmi_dpll_batch_* use (process-wide; default AUTO):
+ *   AUTO     the clause-scan kernel where eligible, else the general kernel
+ *   GENERAL  always the general (occurrence-list) kernel
+ *   SCAN     the clause-scan kernel; an ineligible call fails with SATMI_ERR_ARG */
+#define SATMI_KERNEL_AUTO 0
+#define SATMI_KERNEL_GENERAL 1
+#define SATMI_KERNEL_SCAN 2
+int satmi_dpll_set_kernel(int policy);
+
+/* The launch satmi_dpll_batch_device would make for this batch shape under the
+ * current policy: *kernel = SATMI_KERNEL_SCAN or SATMI_KERNEL_GENERAL, LDS
+ * bytes per wavefront, and wavefronts resident per CU (LDS and registers). */
+int satmi_dpll_plan(int max_vars, int max_clauses, int max_lits, int max_clause_len, int mode, int has_init,
+                    int *kernel, uint64_t *lds_bytes_per_wave, int *waves_per_cu);
 
 #ifdef __cplusplus
 }

@@ -41,11 +41,13 @@
 #include <algorithm>
 #include <climits>
 #include <cstdio>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "common.h"
+#include "dpll_scan.h"
 
 namespace satmi {
 
@@ -875,6 +877,7 @@ struct DeviceWork {
 };
 static std::mutex g_work_mu;
 static std::vector<DeviceWork> g_work;
+static std::atomic<int> g_kernel_policy{SATMI_KERNEL_AUTO};
 
 static int device_work(DeviceWork **out) {
     int dev = 0;
@@ -896,6 +899,51 @@ static int device_work(DeviceWork **out) {
 
 using namespace satmi;
 
+extern "C" int satmi_dpll_set_kernel(int policy) {
+    if (policy != SATMI_KERNEL_AUTO && policy != SATMI_KERNEL_GENERAL && policy != SATMI_KERNEL_SCAN) {
+        set_error("satmi_dpll_set_kernel: unknown policy");
+        return SATMI_ERR_ARG;
+    }
+    g_kernel_policy.store(policy);
+    return SATMI_OK;
+}
+
+extern "C" uint64_t satmi_dpll_scan_lds_bytes(int max_vars, int max_clauses, int max_lits, int max_clause_len) {
+    uint32_t bytes = 0;
+    if (!dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, &bytes)) return 0;
+    return bytes;
+}
+
+extern "C" int satmi_dpll_plan(int max_vars, int max_clauses, int max_lits, int max_clause_len, int mode,
+                               int has_init, int *kernel, uint64_t *lds_bytes_per_wave, int *waves_per_cu) {
+    if (!kernel || !lds_bytes_per_wave || !waves_per_cu) {
+        set_error("satmi_dpll_plan: null output");
+        return SATMI_ERR_ARG;
+    }
+    const int policy = g_kernel_policy.load();
+    uint32_t sb = 0;
+    if (mode == SATMI_MODE_SOUND && !has_init && policy != SATMI_KERNEL_GENERAL &&
+        dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, &sb)) {
+        *kernel = SATMI_KERNEL_SCAN;
+        *lds_bytes_per_wave = sb;
+        return dpll_scan_resident(max_vars, max_clauses, max_clause_len, waves_per_cu);
+    }
+    DpllLayout lay;
+    if (!make_layout(max_vars, max_clauses, max_lits, &lay)) {
+        set_error("satmi_dpll_plan: instance too large for the LDS layout");
+        return SATMI_ERR_TOO_LARGE;
+    }
+    *kernel = SATMI_KERNEL_GENERAL;
+    *lds_bytes_per_wave = lay.bytes;
+    int best = 0;
+    for (int wpg : {4, 2, 1}) {
+        const int wgs = std::min(16, (int)((160u * 1024u) / (lay.bytes * (uint32_t)wpg)));
+        if (wgs >= 1) best = std::max(best, std::min(32, wgs * wpg));
+    }
+    *waves_per_cu = best;
+    return SATMI_OK;
+}
+
 extern "C" uint64_t satmi_dpll_lds_bytes(int max_vars, int max_clauses, int max_lits) {
     DpllLayout lay;
     if (!make_layout(max_vars, max_clauses, max_lits, &lay)) return 0;
@@ -905,7 +953,8 @@ extern "C" uint64_t satmi_dpll_lds_bytes(int max_vars, int max_clauses, int max_
 extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_clause_begin,
                                        const int32_t *d_clause_lit_begin, const int32_t *d_lits,
                                        const int32_t *d_inst_nvars, int max_vars, int max_clauses,
-                                       int max_lits, const int32_t *d_init_begin, const int32_t *d_init_lits,
+                                       int max_lits, int max_clause_len, const int32_t *d_init_begin,
+                                       const int32_t *d_init_lits,
                                        int mode, int64_t max_solutions, int64_t node_limit,
                                        double time_limit_s, int sol_cap, int sol_stride, int32_t *d_status,
                                        int64_t *d_counters, int32_t *d_sol_len, int32_t *d_sol_lits,
@@ -928,6 +977,51 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         return SATMI_ERR_ARG;
     }
     if (num_instances == 0) return SATMI_OK;
+    // SOUND mode without a caller assignment: the clause-scan kernel
+    // (dpll_scan.hip) when the batch shape fits it, unless policy says otherwise
+    const int policy = g_kernel_policy.load();
+    const bool scan_ok = mode == SATMI_MODE_SOUND && !d_init_begin && policy != SATMI_KERNEL_GENERAL &&
+                         dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, nullptr);
+    if (policy == SATMI_KERNEL_SCAN && !scan_ok) {
+        set_error("satmi_dpll_batch_device: SATMI_KERNEL_SCAN policy but the batch is not eligible (SOUND mode, "
+                  "no caller assignment, clause lengths 1..5, <= 2047 variables)");
+        return SATMI_ERR_ARG;
+    }
+    if (scan_ok) {
+        DeviceWork *w = nullptr;
+        int rc = device_work(&w);
+        if (rc) return rc;
+        int dev = 0, cus = 256;
+        SATMI_HIP(hipGetDevice(&dev));
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        ScanLaunch Lc;
+        Lc.num_instances = num_instances;
+        Lc.inst_clause_begin = d_inst_clause_begin;
+        Lc.clause_lit_begin = d_clause_lit_begin;
+        Lc.lits = d_lits;
+        Lc.inst_nvars = d_inst_nvars;
+        Lc.max_vars = max_vars;
+        Lc.max_clauses = max_clauses;
+        Lc.max_lits = max_lits;
+        Lc.max_clause_len = max_clause_len;
+        Lc.max_solutions = max_solutions;
+        Lc.node_limit = node_limit;
+        Lc.time_limit_ticks = time_limit_s > 0 ? (uint64_t)(time_limit_s * w->ticks_per_s) : 0;
+        Lc.sol_cap = sol_cap;
+        Lc.sol_stride = sol_stride;
+        Lc.status = d_status;
+        Lc.counters = d_counters;
+        Lc.sol_len = d_sol_len;
+        Lc.sol_lits = d_sol_lits;
+        Lc.root_len = d_root_len;
+        Lc.root_lits = d_root_lits;
+        Lc.work_counter = w->counter;
+        Lc.num_cus = cus;
+        Lc.stream = (hipStream_t)stream;
+        SATMI_HIP(hipMemsetAsync(w->counter, 0, sizeof(uint32_t), Lc.stream));
+        return dpll_scan_launch(Lc);
+    }
     DpllLayout lay;
     if (!make_layout(max_vars, max_clauses, max_lits, &lay)) {
         set_error("satmi_dpll_batch_device: instance too large for the LDS layout (vars <= 32767, "
@@ -1003,7 +1097,14 @@ extern "C" int satmi_dpll_batch_host(int num_instances, const int32_t *h_inst_cl
     if (num_instances == 0) return SATMI_OK;
     const int C = h_inst_clause_begin[num_instances];
     const int Ltot = h_clause_lit_begin[C];
-    int max_vars = 0, max_clauses = 0, max_lits = 0;
+    int max_vars = 0, max_clauses = 0, max_lits = 0, max_len = 0, min_len = INT_MAX;
+    for (int c = 0; c < C; ++c) {
+        const int len = h_clause_lit_begin[c + 1] - h_clause_lit_begin[c];
+        max_len = std::max(max_len, len);
+        min_len = std::min(min_len, len);
+    }
+    // the scan kernel needs every clause non-empty: report 0 (unknown) otherwise
+    const int max_clause_len = (C > 0 && min_len >= 1) ? max_len : 0;
     for (int b = 0; b < num_instances; ++b) {
         const int cb = h_inst_clause_begin[b], ce = h_inst_clause_begin[b + 1];
         max_clauses = std::max(max_clauses, ce - cb);
@@ -1056,7 +1157,7 @@ extern "C" int satmi_dpll_batch_host(int num_instances, const int32_t *h_inst_cl
         rc = satmi_dpll_batch_device(
             num_instances, (const int32_t *)(d + o_icb), (const int32_t *)(d + o_clb),
             (const int32_t *)(d + o_lits), (const int32_t *)(d + o_nv), max_vars, max_clauses, max_lits,
-            h_init_begin ? (const int32_t *)(d + o_ib) : nullptr,
+            max_clause_len, h_init_begin ? (const int32_t *)(d + o_ib) : nullptr,
             h_init_begin ? (const int32_t *)(d + o_il) : nullptr, mode, max_solutions, node_limit,
             time_limit_s, sol_cap, sol_stride, (int32_t *)(d + o_st), (int64_t *)(d + o_ctr),
             (int32_t *)(d + o_sl), (int32_t *)(d + o_sol), (int32_t *)(d + o_rl), (int32_t *)(d + o_rlits), s);

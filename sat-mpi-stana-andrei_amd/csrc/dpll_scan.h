@@ -1,0 +1,35 @@
+// dpll_scan.h -- launch interface of the clause-scan DPLL kernel (dpll_scan.hip),
+// the SOUND-mode fast path behind satmi_dpll_batch_device (dpll.hip dispatches).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace satmi {
+
+struct ScanLaunch {
+    int num_instances;
+    const int32_t *inst_clause_begin, *clause_lit_begin, *lits, *inst_nvars;
+    int max_vars, max_clauses, max_lits, max_clause_len;
+    int64_t max_solutions, node_limit;
+    uint64_t time_limit_ticks;
+    int sol_cap, sol_stride;
+    int32_t *status;
+    int64_t *counters;
+    int32_t *sol_len, *sol_lits, *root_len, *root_lits;
+    uint32_t *work_counter;
+    int num_cus;
+    hipStream_t stream;
+};
+
+// Can the scan kernel take a batch of this shape (SOUND mode, no caller
+// assignment)?  Fills *lds_bytes with the per-wave LDS it would use.
+bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_clause_len, uint32_t *lds_bytes);
+
+// Waves of the scan kernel resident per CU for this shape (LDS and registers).
+int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu);
+
+// Launch on L.stream (asynchronous).  The caller has checked eligibility and
+// zeroed *L.work_counter on the stream.
+int dpll_scan_launch(const ScanLaunch &L);
+
+}  // namespace satmi

@@ -1,0 +1,702 @@
+// dpll_scan.hip -- batched DPLL for gfx950, SOUND mode: the clause-scan kernel.
+//
+// Same procedure and counters as dpll_batch_kernel (dpll.hip) in
+// SATMI_MODE_SOUND -- dpll_optimized (REF.py:133-214) with each branch literal
+// applied as a unit clause -- in a formulation built for the CDNA4 issue model
+// instead of for minimal work:
+//
+//   * The only mutable state of the formula is one word per literal code,
+//     lv[code] (free / true / false, see LV_*).  There is no per-clause state:
+//     the reference's reduced formula (its filtered Python lists) is
+//     *re-derived* by scanning the packed clauses, 64 clauses per wave step.
+//     A clause is one LDS word (<= 3 literal codes of 10 bits, or <= 5 of 12
+//     bits); the SUM of its literals' state words is the reduced clause:
+//     satisfied or not, its length, and (length 1) its unit literal.
+//   * unit_propagate (REF.py:139-165): a scan collects the unit clauses in
+//     clause order (ballot + popcount compaction) -- exactly REF.py:143's
+//     snapshot.  The snapshot is assigned at once, the first occurrence of a
+//     variable winning (LDS atomicMin of the snapshot index: the `if var in a`
+//     rule of REF.py:149-152).  The next scan builds the next snapshot and
+//     sees emptied clauses; an emptied clause was emptied by the
+//     latest-stamped of its literals, so the reference's stopping unit is the
+//     minimum of those stamps, and the assignments stamped after it are
+//     dropped -- counters match the reference one for one.
+//   * Backtracking clears the state words of the popped trail entries and
+//     nothing else: there is no clause state to undo.
+//   * Pure literals / branching (REF.py:174-208): one scan adds every free
+//     occurrence of an active clause into per-variable counters and keeps the
+//     first position (the dict order of literal_sign / var_counts).
+//
+// A scan step is K independent LDS gathers and K-1 adds per lane, so the
+// kernel is VALU/LDS-issue bound with short dependency chains, and the
+// per-wave LDS image is small (n=100, m=426: 5.3 KB).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+
+#include "common.h"
+#include "dpll_scan.h"
+
+// minimum waves per SIMD the register allocation must allow (launch bounds)
+#ifndef SATMI_SCAN_WAVES_PER_SIMD
+#define SATMI_SCAN_WAVES_PER_SIMD 7
+#endif
+
+namespace satmi {
+namespace {
+
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr uint32_t PHASE_BIT = 0x8000u;
+
+// Literal state word lv[code] (code = v << 1 | negative).  The sum of a
+// clause's words: bits 0-2 = free occurrences (REF.py's len(c)), bits 3-7 =
+// 8 x true occurrences (!= 0: the reference dropped the clause), bits 8+ = sum
+// of the free codes (exactly one free occurrence: the unit literal).  Code 0
+// (variable 0, positive) pads short clauses and is pinned false; code 1 is
+// pinned true and fills the dummy clauses that round the clause array up to
+// whole 64-clause chunks.
+constexpr uint32_t LV_TRUE = 8u, LV_FALSE = 0u;
+constexpr uint32_t CODE_PAD = 0u, CODE_DUMMY = 1u;
+__device__ __forceinline__ uint32_t lv_free(uint32_t code) { return 1u + (code << 8); }
+__device__ __forceinline__ bool sum_true(uint32_t s) { return (s & 0xF8u) != 0u; }
+__device__ __forceinline__ uint32_t sum_nfree(uint32_t s) { return s & 7u; }
+
+template <int K>
+struct Pack;
+template <>
+struct Pack<3> {
+    using W = uint32_t;
+    static constexpr int BITS = 10;
+    static constexpr int MAXV = 511;
+    static constexpr int UNROLL = 4;
+};
+template <>
+struct Pack<5> {
+    using W = uint64_t;
+    static constexpr int BITS = 12;
+    static constexpr int MAXV = 2047;
+    static constexpr int UNROLL = 2;
+};
+
+template <int K>
+__device__ __forceinline__ uint32_t field(typename Pack<K>::W w, int j) {
+    return (uint32_t)(w >> (Pack<K>::BITS * j)) & ((1u << Pack<K>::BITS) - 1u);
+}
+
+struct ScanLayout {
+    uint32_t cls, lv, ts, cnt, first, trail, fvar, ftrail, scratch, bytes;
+    int32_t mcap, ncap;
+};
+
+struct ScanArgs {
+    const int32_t *inst_clause_begin, *clause_lit_begin, *lits, *inst_nvars;
+    int32_t num_instances, sol_cap, sol_stride;
+    int64_t max_solutions, node_limit;
+    uint64_t time_limit_ticks;
+    int32_t *status;
+    int64_t *counters;
+    int32_t *sol_len, *sol_lits, *root_len, *root_lits;
+    uint32_t *work_counter;
+    ScanLayout lay;
+};
+
+template <int K>
+struct SLds {
+    typename Pack<K>::W *cls;   // [mcap rounded up to 64]  packed literal codes per clause
+    uint32_t *lv;               // [2(ncap+1)]  literal state words
+    uint32_t *ts;               // [ncap+1]  snapshot index of the assignment in the running batch
+    uint32_t *cnt;              // [ncap+1]  free occurrences in active clauses, pos | neg << 16
+    uint32_t *first;            // [ncap+1]  first free occurrence, position c << 3 | slot
+    uint16_t *trail;            // [ncap+1]  assignment order (literal codes) == dict insertion order
+    uint16_t *fvar;             // [ncap+1]  decision frames: var | PHASE_BIT once False runs
+    uint16_t *ftrail;           // [ncap+1]  trail length before the decision
+    uint16_t *snap;             // scratch:  unit-clause snapshot (propagation)
+    uint32_t *plist;            // scratch:  pure-literal positions (analysis), aliases snap
+};
+
+// literal `code` becomes true: one 8-byte store sets both literals of its variable
+__device__ __forceinline__ void lv_assign(uint32_t *lv, uint32_t code) {
+    *(uint64_t *)(lv + (code & ~1u)) = (code & 1u) ? ((uint64_t)LV_TRUE << 32) : (uint64_t)LV_TRUE;
+}
+__device__ __forceinline__ void lv_clear(uint32_t *lv, uint32_t v) {
+    *(uint64_t *)(lv + 2 * v) = (uint64_t)lv_free(2 * v) | ((uint64_t)lv_free(2 * v + 1) << 32);
+}
+__device__ __forceinline__ bool var_free(const uint32_t *lv, uint32_t v) { return (lv[2 * v] & 1u) != 0u; }
+
+// Apply f(c, w, x) to every clause c (w its packed word, x[j] the state word of
+// its slot j), one 64-clause chunk per lane step; the loads of U chunks are
+// issued before any is used.  mpad is a multiple of 64 (dummy clauses are
+// always satisfied).
+template <int K, int U, typename F>
+__device__ __forceinline__ void for_chunks(const SLds<K> &S, int mpad, F &&f) {
+    using W = typename Pack<K>::W;
+    const int ln = lane_id();
+    int c0 = 0;
+    for (; c0 + 64 * U <= mpad; c0 += 64 * U) {
+        W w[U];
+        uint32_t x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = S.cls[c0 + 64 * u + ln];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[u][j] = S.lv[field<K>(w[u], j)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) f(c0 + 64 * u + ln, w[u], x[u]);
+    }
+    for (; c0 < mpad; c0 += 64) {
+        const W w = S.cls[c0 + ln];
+        uint32_t x[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = S.lv[field<K>(w, j)];
+        f(c0 + ln, w, x);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t clause_sum(const uint32_t (&x)[K]) {
+    uint32_t s = x[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) s += x[j];
+    return s;
+}
+
+// Scan for unit_propagate: the unit-clause snapshot (REF.py:143), in clause
+// order, into S.snap; *any_empty: some clause has no free literal left.
+template <int K>
+__device__ int scan_units(const SLds<K> &S, int mpad, bool *any_empty) {
+    using W = typename Pack<K>::W;
+    const uint64_t lt = lanemask_lt();
+    int nu = 0;
+    bool emp = false;
+    for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int, W, const uint32_t(&x)[K]) {
+        const uint32_t s = clause_sum<K>(x);
+        const bool open = !sum_true(s);
+        const uint32_t nf = sum_nfree(s);
+        emp |= open && nf == 0u;
+        const bool unit = open && nf == 1u;
+        const uint64_t mk = __ballot(unit);
+        if (unit) S.snap[nu + __popcll(mk & lt)] = (uint16_t)(s >> 8);
+        nu += __popcll(mk);
+    });
+    wave_sync();
+    *any_empty = __ballot(emp) != 0ull;
+    return nu;
+}
+
+// The snapshot index whose assignment emptied a clause first: an emptied
+// clause was emptied by the latest-stamped of its literals (REF.py:161-162).
+template <int K>
+__device__ int empty_time(const SLds<K> &S, int mpad) {
+    using W = typename Pack<K>::W;
+    int e = INT_MAX;
+    for_chunks<K, 1>(S, mpad, [&](int, W w, const uint32_t(&x)[K]) {
+        const uint32_t s = clause_sum<K>(x);
+        if (!sum_true(s) && sum_nfree(s) == 0u) {
+            int t = -1;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint32_t code = field<K>(w, j);
+                const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : NONE32;
+                if (st != NONE32) t = max(t, (int)st);
+            }
+            e = min(e, t);
+        }
+    });
+    return wave_min_i32(e);
+}
+
+// unit_propagate (REF.py:139-165) from the snapshot S.snap[0, nu).  Returns
+// true on conflict; `tl` ends where the reference stops (the assignments it
+// made, including the one that emptied a clause).  `dec`: the first batch is
+// the decision literal, which REF.py's counters do not count as a propagation.
+template <int K>
+__device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec, int64_t &props,
+                          int64_t &rounds) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    while (nu > 0) {
+        ++rounds;
+        const int rs = tl;
+        for (int k0 = 0; k0 < nu; k0 += 64) {
+            const int k = k0 + ln;
+            const bool valid = k < nu;
+            const uint32_t code = valid ? (uint32_t)S.snap[k] : 0u;
+            const uint32_t v = code >> 1;
+            if (valid) atomicMin(&S.ts[v], (uint32_t)k);
+            wave_sync();
+            const bool first = valid && S.ts[v] == (uint32_t)k;
+            const uint64_t mk = __ballot(first);
+            if (first) {
+                S.trail[tl + __popcll(mk & lt)] = (uint16_t)code;
+                lv_assign(S.lv, code);
+            }
+            tl += __popcll(mk);
+        }
+        wave_sync();
+        const int nassign = tl - rs;
+        bool emptied = false;
+        const int nu_next = scan_units<K>(S, mpad, &emptied);
+        if (emptied) {
+            // the reference stopped at snapshot index e: keep the prefix of the
+            // batch stamped <= e (the batch is in stamp order)
+            const int e = empty_time<K>(S, mpad);
+            int keep = 0;
+            for (int i0 = rs; i0 < tl; i0 += 64) {
+                const int i = i0 + ln;
+                const bool p = i < tl && S.ts[S.trail[i] >> 1] <= (uint32_t)e;
+                keep += __popcll(__ballot(p));
+            }
+            const int cut = rs + keep;
+            wave_sync();
+            for (int i = rs + ln; i < tl; i += 64) {
+                const uint32_t v = S.trail[i] >> 1;
+                S.ts[v] = NONE32;
+                if (i >= cut) lv_clear(S.lv, v);
+            }
+            wave_sync();
+            tl = cut;
+            props += keep - (dec ? 1 : 0);
+            return true;
+        }
+        for (int i = rs + ln; i < tl; i += 64) S.ts[S.trail[i] >> 1] = NONE32;
+        wave_sync();
+        props += nassign - (dec && nassign > 0 ? 1 : 0);
+        dec = false;
+        if (nassign == 0) break;   // `changed` stayed False (REF.py:141-142)
+        nu = nu_next;
+    }
+    return false;
+}
+
+// literal_sign / var_counts scan (REF.py:174-179, :198-203): every free
+// occurrence in an active clause is counted per variable, and the first
+// position kept.  Returns the number of active clauses (0: REF.py:170-171).
+// Within an active clause the atomics run for every slot -- a falsified slot
+// adds 0 / mins NONE32, padding hits variable 0 (never read) -- so there is
+// no branch per slot.
+template <int K>
+__device__ int scan_counts(const SLds<K> &S, int mpad) {
+    using W = typename Pack<K>::W;
+    int nact = 0;
+    for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int c, W w, const uint32_t(&x)[K]) {
+        const bool act = !sum_true(clause_sum<K>(x));
+        nact += __popcll(__ballot(act));
+        if (act) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint32_t code = field<K>(w, j);
+                const bool fr = (x[j] & 1u) != 0u;
+                atomicAdd(&S.cnt[code >> 1], fr ? ((code & 1u) ? 0x10000u : 1u) : 0u);
+                atomicMin(&S.first[code >> 1], fr ? (((uint32_t)c << 3) | (uint32_t)j) : NONE32);
+            }
+        }
+    });
+    wave_sync();
+    return nact;
+}
+
+struct Choice {
+    int npure;
+    uint32_t best_var;   // 0 = no unassigned variable occurs (REF.py:205)
+};
+
+// pure_literals (REF.py:181-184) into plist (first positions), else the
+// branching variable: max(var_counts.items(), key=count), the first maximal
+// key in dict order (REF.py:208).  Clears cnt / first for the next scan.
+template <int K>
+__device__ Choice choose(const SLds<K> &S, int n) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    int npure = 0;
+    uint32_t maxc = 0;
+    for (int v0 = 1; v0 <= n; v0 += 64) {
+        const int v = v0 + ln;
+        bool pure = false;
+        uint32_t f = NONE32;
+        if (v <= n && var_free(S.lv, (uint32_t)v)) {
+            const uint32_t c = S.cnt[v];
+            const uint32_t p = c & 0xFFFFu, q = c >> 16;
+            maxc = max(maxc, p + q);
+            pure = (p + q) != 0u && (p == 0u || q == 0u);
+            f = S.first[v];
+        }
+        const uint64_t mk = __ballot(pure);
+        if (pure) S.plist[npure + __popcll(mk & lt)] = f;
+        npure += __popcll(mk);
+    }
+    maxc = wave_max_u32(maxc);
+    uint32_t best = 0;
+    if (npure == 0 && maxc > 0) {
+        uint32_t bestf = NONE32;
+        for (int v0 = 1; v0 <= n; v0 += 64) {
+            const int v = v0 + ln;
+            if (v <= n && var_free(S.lv, (uint32_t)v)) {
+                const uint32_t c = S.cnt[v];
+                if ((c & 0xFFFFu) + (c >> 16) == maxc) bestf = min(bestf, S.first[v]);
+            }
+        }
+        bestf = wave_min_u32(bestf);
+        best = uniform_u32(field<K>(S.cls[bestf >> 3], (int)(bestf & 7u)) >> 1);
+    }
+    for (int v = ln; v <= n; v += 64) {
+        S.cnt[v] = 0u;
+        S.first[v] = NONE32;
+    }
+    wave_sync();
+    return {npure, best};
+}
+
+// Append the pure literals in first-occurrence order (REF.py:187-189); the
+// literal at a pure variable's first position carries its (only) sign.
+template <int K>
+__device__ int assign_pures(const SLds<K> &S, int npure, int tl) {
+    const int ln = lane_id();
+    for (int i0 = 0; i0 < npure; i0 += 64) {
+        const int i = i0 + ln;
+        const uint32_t my = i < npure ? S.plist[i] : NONE32;
+        int rank = 0;
+        for (int j = 0; j < npure; ++j) rank += S.plist[j] < my ? 1 : 0;
+        if (i < npure) {
+            const uint32_t code = field<K>(S.cls[my >> 3], (int)(my & 7u));
+            S.trail[tl + rank] = (uint16_t)code;
+            lv_assign(S.lv, code);
+        }
+    }
+    wave_sync();
+    return tl + npure;
+}
+
+template <int K>
+__device__ void store_assignment(const SLds<K> &S, int tl, int32_t *out) {
+    for (int i = lane_id(); i < tl; i += 64) {
+        const uint32_t code = S.trail[i];
+        const int v = (int)(code >> 1);
+        out[i] = (code & 1u) ? -v : v;
+    }
+}
+
+enum { ST_PROPAGATE = 0, ST_ANALYZE = 1, ST_BACKTRACK = 2, ST_DONE = 3 };
+
+template <int K>
+__device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
+    using W = typename Pack<K>::W;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    const int ln = lane_id();
+    const int cb = A.inst_clause_begin[b], ce = A.inst_clause_begin[b + 1];
+    const int m = ce - cb;
+    const int mpad = (m + 63) & ~63;
+    const int L = A.clause_lit_begin[ce] - A.clause_lit_begin[cb];
+    const int n = A.inst_nvars[b];
+    int64_t *ctr = A.counters + (int64_t)b * SATMI_NCOUNTERS;
+    bool bad = m > A.lay.mcap || n > A.lay.ncap || n < 0 || L > 65535;
+    if (!bad) {
+        // ---- stage: pack each clause's literal codes into one word
+        for (int c = ln; c < mpad; c += 64) {
+            W w = (W)CODE_DUMMY;
+            if (c < m) {
+                const int j0 = A.clause_lit_begin[cb + c], j1 = A.clause_lit_begin[cb + c + 1];
+                const int len = j1 - j0;
+                w = 0;
+                if (len < 1 || len > K) {
+                    bad = true;
+                } else {
+                    for (int j = 0; j < len; ++j) {
+                        const int x = A.lits[j0 + j];
+                        const uint32_t v = (uint32_t)(x < 0 ? -x : x);
+                        if (v == 0u || v > (uint32_t)n) bad = true;
+                        w |= (W)((v << 1) | (x < 0 ? 1u : 0u)) << (Pack<K>::BITS * j);
+                    }
+                }
+            }
+            S.cls[c] = w;
+        }
+        for (int v = ln; v <= n; v += 64) {
+            if (v == 0) {
+                S.lv[CODE_PAD] = LV_FALSE;
+                S.lv[CODE_DUMMY] = LV_TRUE;
+            } else {
+                lv_clear(S.lv, (uint32_t)v);
+            }
+            S.ts[v] = NONE32;
+            S.cnt[v] = 0u;
+            S.first[v] = NONE32;
+        }
+    }
+    if (__ballot(bad)) {
+        if (ln < SATMI_NCOUNTERS) ctr[ln] = 0;
+        if (ln == 0) {
+            A.status[b] = SATMI_DPLL_TOO_LARGE;
+            if (A.root_len) A.root_len[b] = 0;
+        }
+        return;
+    }
+    wave_sync();
+
+    // root snapshot: the input's unit clauses in order (no clause is empty yet)
+    bool root_empty = false;
+    int nu = scan_units<K>(S, mpad, &root_empty);
+    int64_t nodes = 1, decisions = 0, props = 0, pures = 0, conflicts = 0, sols = 0, rounds = 0;
+    int depth = 0, tl = 0;
+    int status = SATMI_DPLL_EXHAUSTED;
+    bool dec_round = false, at_root = true;
+    int state = ST_PROPAGATE;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+
+    while (state != ST_DONE) {
+        if (state == ST_PROPAGATE) {
+            const bool conflict = propagate<K>(S, mpad, tl, nu, dec_round, props, rounds);
+            dec_round = false;
+            if (at_root) {
+                at_root = false;
+                if (A.root_lits) store_assignment<K>(S, tl, A.root_lits + (int64_t)b * A.sol_stride);
+                if (A.root_len && ln == 0) A.root_len[b] = tl;
+            }
+            if (conflict) {
+                ++conflicts;
+                state = ST_BACKTRACK;
+            } else {
+                state = ST_ANALYZE;
+            }
+            continue;
+        }
+        if (state == ST_ANALYZE) {
+            bool leaf = false;
+            Choice r{0, 0u};
+            if (scan_counts<K>(S, mpad) == 0) {
+                leaf = true;                                   // REF.py:170-171
+            } else {
+                r = choose<K>(S, n);
+                if (r.npure == 0 && r.best_var == 0u) leaf = true;   // REF.py:205-206
+            }
+            if (!leaf && r.npure > 0) {                        // REF.py:186-195
+                tl = assign_pures<K>(S, r.npure, tl);
+                pures += r.npure;
+                ++nodes;                                       // recursive call; its unit_propagate is a no-op
+            } else if (!leaf) {                                // REF.py:208-213, as formula + [[var]]
+                const uint32_t v = r.best_var;
+                if (ln == 0) {
+                    S.fvar[depth] = (uint16_t)v;
+                    S.ftrail[depth] = (uint16_t)tl;
+                    S.snap[0] = (uint16_t)(v << 1);            // True first
+                }
+                ++depth;
+                ++decisions;
+                ++nodes;
+                nu = 1;
+                dec_round = true;
+                state = ST_PROPAGATE;
+                wave_sync();
+            }
+            if (leaf) {
+                if (sols < A.sol_cap) {
+                    store_assignment<K>(S, tl, A.sol_lits + ((int64_t)b * A.sol_cap + sols) * A.sol_stride);
+                    if (ln == 0) A.sol_len[(int64_t)b * A.sol_cap + sols] = tl;
+                }
+                ++sols;
+                if (A.max_solutions > 0 && sols >= A.max_solutions) {
+                    status = SATMI_DPLL_STOPPED;
+                    state = ST_DONE;
+                } else {
+                    state = ST_BACKTRACK;
+                }
+            }
+        }
+        if (state == ST_BACKTRACK) {
+            state = ST_DONE;
+            while (depth > 0) {
+                const int top = depth - 1;
+                const uint32_t fv = uniform_u32(S.fvar[top]);
+                const int ft = uniform_i32(S.ftrail[top]);
+                for (int i = ft + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
+                tl = ft;
+                wave_sync();
+                if (!(fv & PHASE_BIT)) {
+                    if (ln == 0) {
+                        S.fvar[top] = (uint16_t)(fv | PHASE_BIT);
+                        S.snap[0] = (uint16_t)((fv << 1) | 1u);    // False
+                    }
+                    ++decisions;
+                    ++nodes;
+                    nu = 1;
+                    dec_round = true;
+                    state = ST_PROPAGATE;
+                    wave_sync();
+                    break;
+                }
+                --depth;
+            }
+        }
+        if (state != ST_DONE) {
+            if (A.node_limit > 0 && nodes > A.node_limit) {
+                status = SATMI_DPLL_NODE_LIMIT;
+                state = ST_DONE;
+            } else if (A.time_limit_ticks && __builtin_amdgcn_s_memrealtime() - t0 > A.time_limit_ticks) {
+                status = SATMI_DPLL_TIMEOUT;
+                state = ST_DONE;
+            }
+        }
+    }
+    if (ln == 0) {
+        A.status[b] = status;
+        ctr[SATMI_CTR_NODES] = nodes;
+        ctr[SATMI_CTR_DECISIONS] = decisions;
+        ctr[SATMI_CTR_UNIT_PROPS] = props;
+        ctr[SATMI_CTR_PURE] = pures;
+        ctr[SATMI_CTR_CONFLICTS] = conflicts;
+        ctr[SATMI_CTR_SOLUTIONS] = sols;
+        ctr[SATMI_CTR_ROUNDS] = rounds;
+        ctr[SATMI_CTR_TICKS] = (int64_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+    }
+}
+
+// Persistent grid: waves pull instance indices from a global counter until the
+// batch is drained (search-tree sizes differ by orders of magnitude).
+template <int K>
+__global__ void __launch_bounds__(256, SATMI_SCAN_WAVES_PER_SIMD) dpll_scan_kernel(ScanArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *base = smem + (size_t)(threadIdx.x >> 6) * A.lay.bytes;
+    SLds<K> S;
+    S.cls = (typename Pack<K>::W *)(base + A.lay.cls);
+    S.lv = (uint32_t *)(base + A.lay.lv);
+    S.ts = (uint32_t *)(base + A.lay.ts);
+    S.cnt = (uint32_t *)(base + A.lay.cnt);
+    S.first = (uint32_t *)(base + A.lay.first);
+    S.trail = (uint16_t *)(base + A.lay.trail);
+    S.fvar = (uint16_t *)(base + A.lay.fvar);
+    S.ftrail = (uint16_t *)(base + A.lay.ftrail);
+    S.snap = (uint16_t *)(base + A.lay.scratch);
+    S.plist = (uint32_t *)(base + A.lay.scratch);
+    for (;;) {
+        uint32_t b = 0;
+        if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
+        b = uniform_u32(b);
+        if (b >= (uint32_t)A.num_instances) break;
+        solve_instance<K>(A, S, (int)b);
+        wave_sync();
+    }
+}
+
+uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+
+int pick_k(int max_vars, int max_clause_len) {
+    if (max_clause_len < 1 || max_clause_len > 5) return 0;
+    if (max_clause_len <= 3 && max_vars <= Pack<3>::MAXV) return 3;
+    if (max_vars <= Pack<5>::MAXV) return 5;
+    return 0;
+}
+
+bool make_layout(int K, int max_vars, int max_clauses, ScanLayout *lay) {
+    if (max_vars < 0 || max_clauses < 0 || max_clauses > 65534) return false;
+    const uint32_t N = (uint32_t)max_vars + 1, M = (uint32_t)max_clauses + 1;
+    const uint32_t Mpad = ((uint32_t)max_clauses + 63u) & ~63u;
+    uint32_t o = 0;
+    lay->cls = o;     o = align16(o + (K == 3 ? 4u : 8u) * Mpad);
+    lay->lv = o;      o = align16(o + 8 * N);
+    lay->ts = o;      o = align16(o + 4 * N);
+    lay->cnt = o;     o = align16(o + 4 * N);
+    lay->first = o;   o = align16(o + 4 * N);
+    lay->trail = o;   o = align16(o + 2 * N);
+    lay->fvar = o;    o = align16(o + 2 * N);
+    lay->ftrail = o;  o = align16(o + 2 * N);
+    lay->scratch = o; o = align16(o + std::max(2 * M, 4 * N));
+    lay->bytes = o;
+    lay->mcap = max_clauses;
+    lay->ncap = max_vars;
+    return o <= 160u * 1024u;
+}
+
+// Launch shape: the workgroup size that keeps the most waves resident under
+// LDS (<= 32 waves, <= 16 workgroups per CU) and the kernel's register budget
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor).
+int scan_plan(int K, const ScanLayout &lay, int *waves_per_wg, int *wg_per_cu) {
+    const void *fn = K == 3 ? (const void *)dpll_scan_kernel<3> : (const void *)dpll_scan_kernel<5>;
+    int best = 0;
+    for (int wpg : {4, 2, 1}) {
+        const uint32_t wg_lds = lay.bytes * (uint32_t)wpg;
+        int wgs = std::min(16, (int)((160u * 1024u) / wg_lds));
+        if (wgs < 1) continue;
+        if (wg_lds > 64u * 1024u)
+            SATMI_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wg_lds));
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64 * wpg, wg_lds) == hipSuccess && occ > 0)
+            wgs = std::min(wgs, occ);
+        const int waves = std::min(32, wgs * wpg);
+        if (waves > best) {
+            best = waves;
+            *waves_per_wg = wpg;
+            *wg_per_cu = std::max(1, std::min(wgs, 32 / wpg));
+        }
+    }
+    if (!best) {
+        set_error("dpll_scan: no resident workgroup shape");
+        return SATMI_ERR_TOO_LARGE;
+    }
+    return SATMI_OK;
+}
+
+}  // namespace
+
+bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_clause_len, uint32_t *lds_bytes) {
+    const int K = pick_k(max_vars, max_clause_len);
+    if (!K || max_lits > 65535) return false;
+    ScanLayout lay;
+    if (!make_layout(K, max_vars, max_clauses, &lay)) return false;
+    if (lds_bytes) *lds_bytes = lay.bytes;
+    return true;
+}
+
+int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu) {
+    const int K = pick_k(max_vars, max_clause_len);
+    ScanLayout lay;
+    if (!K || !make_layout(K, max_vars, max_clauses, &lay)) return SATMI_ERR_ARG;
+    int wpg = 1, wgc = 1;
+    const int rc = scan_plan(K, lay, &wpg, &wgc);
+    if (rc) return rc;
+    *waves_per_cu = wpg * wgc;
+    return SATMI_OK;
+}
+
+int dpll_scan_launch(const ScanLaunch &L) {
+    const int K = pick_k(L.max_vars, L.max_clause_len);
+    ScanLayout lay;
+    if (!K || !make_layout(K, L.max_vars, L.max_clauses, &lay)) {
+        set_error("dpll_scan_launch: batch shape not eligible for the scan kernel");
+        return SATMI_ERR_ARG;
+    }
+    int waves_per_wg = 1, wg_per_cu = 1;
+    const int prc = scan_plan(K, lay, &waves_per_wg, &wg_per_cu);
+    if (prc) return prc;
+    const uint32_t wg_lds = lay.bytes * (uint32_t)waves_per_wg;
+    const int need = (L.num_instances + waves_per_wg - 1) / waves_per_wg;
+    const int grid = std::max(1, std::min(need, L.num_cus * wg_per_cu));
+
+    ScanArgs A;
+    A.inst_clause_begin = L.inst_clause_begin;
+    A.clause_lit_begin = L.clause_lit_begin;
+    A.lits = L.lits;
+    A.inst_nvars = L.inst_nvars;
+    A.num_instances = L.num_instances;
+    A.sol_cap = L.sol_cap;
+    A.sol_stride = L.sol_stride;
+    A.max_solutions = L.max_solutions;
+    A.node_limit = L.node_limit;
+    A.time_limit_ticks = L.time_limit_ticks;
+    A.status = L.status;
+    A.counters = L.counters;
+    A.sol_len = L.sol_len;
+    A.sol_lits = L.sol_lits;
+    A.root_len = L.root_len;
+    A.root_lits = L.root_lits;
+    A.work_counter = L.work_counter;
+    A.lay = lay;
+    if (K == 3)
+        hipLaunchKernelGGL(dpll_scan_kernel<3>, dim3(grid), dim3(64 * waves_per_wg), wg_lds, L.stream, A);
+    else
+        hipLaunchKernelGGL(dpll_scan_kernel<5>, dim3(grid), dim3(64 * waves_per_wg), wg_lds, L.stream, A);
+    SATMI_HIP(hipGetLastError());
+    return SATMI_OK;
+}
+
+}  // namespace satmi

@@ -20,14 +20,20 @@ COUNTER_NAMES = ("nodes", "decisions", "unit_props", "pure_assigns", "conflicts"
 DPLL_EXHAUSTED, DPLL_STOPPED, DPLL_NODE_LIMIT, DPLL_TIMEOUT, DPLL_TOO_LARGE = range(5)
 STATUS_NAMES = {0: "exhausted", 1: "stopped", 2: "node_limit", 3: "timeout", 4: "too_large"}
 RES_SAT, RES_UNSAT, RES_LIMIT = 1, 0, -1
+KERNEL_AUTO, KERNEL_GENERAL, KERNEL_SCAN = 0, 1, 2
 
 # exported symbols, checked by tests/test_capi_symbols.py against include/satmi.h
 EXPORTED = (
     "satmi_abi_version", "satmi_last_error", "satmi_device_count", "satmi_set_device", "satmi_synchronize",
     "satmi_malloc", "satmi_free", "satmi_memcpy_h2d", "satmi_memcpy_d2h", "satmi_stream_synchronize",
     "satmi_dpll_batch_device", "satmi_dpll_batch_host", "satmi_dpll_lds_bytes", "satmi_resolution_host",
-    "satmi_dp_host",
+    "satmi_dp_host", "satmi_dpll_scan_lds_bytes", "satmi_dpll_set_kernel", "satmi_dpll_plan",
 )
+
+
+def set_kernel(policy):
+    """Process-wide DPLL kernel policy (KERNEL_AUTO / KERNEL_GENERAL / KERNEL_SCAN)."""
+    check(load().satmi_dpll_set_kernel(int(policy)), "satmi_dpll_set_kernel")
 
 
 class SatmiError(RuntimeError):
@@ -65,8 +71,12 @@ def load():
     L.satmi_stream_synchronize.argtypes = [vp]
     L.satmi_dpll_lds_bytes.restype = ctypes.c_uint64
     L.satmi_dpll_lds_bytes.argtypes = [ctypes.c_int] * 3
+    L.satmi_dpll_scan_lds_bytes.restype = ctypes.c_uint64
+    L.satmi_dpll_scan_lds_bytes.argtypes = [ctypes.c_int] * 4
+    L.satmi_dpll_set_kernel.argtypes = [ctypes.c_int]
+    L.satmi_dpll_plan.argtypes = [ctypes.c_int] * 6 + [P(ctypes.c_int), P(ctypes.c_uint64), P(ctypes.c_int)]
     L.satmi_dpll_batch_device.argtypes = [
-        ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
+        ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
         ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, ctypes.c_int, ctypes.c_int,
         vp, vp, vp, vp, vp, vp, vp]
     L.satmi_dpll_batch_host.argtypes = [
@@ -83,6 +93,15 @@ def load():
         getattr(L, name)  # AttributeError here = library/header mismatch
     _lib = L
     return L
+
+
+def plan(max_vars, max_clauses, max_lits, max_clause_len, mode=MODE_SOUND, has_init=False):
+    """(kernel, lds_bytes_per_wave, waves_per_cu) of the launch satmi_dpll_batch_device would make."""
+    k, lds, w = ctypes.c_int(0), ctypes.c_uint64(0), ctypes.c_int(0)
+    check(load().satmi_dpll_plan(int(max_vars), int(max_clauses), int(max_lits), int(max_clause_len), int(mode),
+                                 int(bool(has_init)), ctypes.byref(k), ctypes.byref(lds), ctypes.byref(w)),
+          "satmi_dpll_plan")
+    return k.value, lds.value, w.value
 
 
 def check(rc, what):

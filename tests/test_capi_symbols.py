@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_symbols():
         assert hasattr(lib, name), name
     lib.satmi_abi_version.restype = ctypes.c_int
-    assert lib.satmi_abi_version() == 1
+    assert lib.satmi_abi_version() == 2
 
 
 def test_lds_layout_query():
@@ -38,3 +38,29 @@ def test_lds_layout_query():
     assert 0 < b100 < 16 * 1024
     assert L.satmi_dpll_lds_bytes(40000, 10, 10) == 0      # var codes are 15-bit
     assert L.satmi_dpll_lds_bytes(100, 100000, 100) == 0   # clause offsets are 16-bit
+
+
+def test_scan_kernel_eligibility_query():
+    """The clause-scan kernel's LDS image and eligibility (host-side layout only)."""
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("libsatmi.so not built")
+    L = _capi.load()
+    s100 = L.satmi_dpll_scan_lds_bytes(100, 426, 1278, 3)
+    assert 0 < s100 <= 5 * 1024 < L.satmi_dpll_lds_bytes(100, 426, 1278)
+    assert L.satmi_dpll_scan_lds_bytes(200, 4223, 21115, 5) > 0          # configs[4] 5-SAT
+    assert L.satmi_dpll_scan_lds_bytes(600, 100, 300, 3) > 0             # > 511 vars: 12-bit codes
+    assert L.satmi_dpll_scan_lds_bytes(100, 426, 1278, 6) == 0           # clauses of <= 5 literals
+    assert L.satmi_dpll_scan_lds_bytes(100, 426, 1278, 0) == 0           # unknown / empty clause
+    assert L.satmi_dpll_scan_lds_bytes(3000, 426, 1278, 3) == 0          # <= 2047 variables
+    # the plan follows the policy: REF mode and caller assignments use the general kernel
+    assert _capi.plan(100, 426, 1278, 3, _capi.MODE_REF)[0] == _capi.KERNEL_GENERAL
+    assert _capi.plan(100, 426, 1278, 3, _capi.MODE_SOUND, has_init=True)[0] == _capi.KERNEL_GENERAL
+    kern, lds, _ = _capi.plan(100, 426, 1278, 3)
+    assert (kern, lds) == (_capi.KERNEL_SCAN, s100)
+    _capi.set_kernel(_capi.KERNEL_GENERAL)
+    try:
+        assert _capi.plan(100, 426, 1278, 3)[0] == _capi.KERNEL_GENERAL
+    finally:
+        _capi.set_kernel(_capi.KERNEL_AUTO)
+    with pytest.raises(_capi.SatmiError):
+        _capi.set_kernel(7)

@@ -122,3 +122,131 @@ def test_limits_and_too_large():
     hard = cnf.uniform_ksat(1, 250, 1065, 3, seed=3).instance(0)
     r = dpll_batch([hard], mode="sound", max_solutions=0, time_limit=0.05, sol_cap=4)
     assert r.status[0] == _capi.DPLL_TIMEOUT
+
+
+# BASELINE configs[4]: uf250-1065-shaped 3-SAT and random 5-SAT n=200 at the
+# 5-SAT threshold (alpha=21.117, m=4,223 -- the LDS-pressure layout: one wave
+# per CU).  Full searches take 10^6+ calls for this heuristic, so parity is
+# checked on node-capped searches: status, all counters and any model match the
+# oracle bit-exactly at the cap.
+@pytest.mark.parametrize("n,m,k,cap", [(250, 1065, 3, 1500), (200, 4223, 5, 600)])
+def test_configs4_node_capped_parity(n, m, k, cap):
+    B = 6
+    batch = cnf.uniform_ksat(B, n, m, k, seed=4 * n + k)
+    r = dpll_batch(batch, mode="sound", max_solutions=1, node_limit=cap, sol_cap=1)
+    for b in range(B):
+        o = oracle.dpll(batch.instance(b), "sound", max_solutions=1, node_limit=cap, sol_cap=1)
+        assert int(r.status[b]) == o["status"], b
+        got = r.counter_dict(b)
+        for key in CTR:
+            assert got[key] == o["counters"][key], (b, key)
+        assert r.solutions(b)[:1] == o["solutions"][:1]
+
+
+@pytest.mark.parametrize("n,m,k,cap,B", [(250, 1065, 3, 4000, 512), (200, 4223, 5, 1500, 256)])
+def test_configs4_batch_properties(n, m, k, cap, B):
+    batch = cnf.uniform_ksat(B, n, m, k, seed=n + 31 * k)
+    r = dpll_batch(batch, mode="sound", max_solutions=1, node_limit=cap, sol_cap=1)
+    ok = (_capi.DPLL_STOPPED, _capi.DPLL_EXHAUSTED, _capi.DPLL_NODE_LIMIT)
+    for b in range(B):
+        assert int(r.status[b]) in ok
+        nodes = r.counter_dict(b)["nodes"]
+        if r.status[b] == _capi.DPLL_NODE_LIMIT:
+            assert nodes == cap + 1
+        else:
+            assert nodes <= cap
+        if r.num_solutions(b):
+            assert _satisfies(batch.instance(b), r.solutions(b)[0])
+    # exact on a sample, at the batch's own cap
+    for b in (0, B // 2, B - 1):
+        o = oracle.dpll(batch.instance(b), "sound", max_solutions=1, node_limit=cap, sol_cap=1)
+        assert int(r.status[b]) == o["status"]
+        assert r.counter_dict(b) == {**r.counter_dict(b), **{k_: o["counters"][k_] for k_ in CTR}}
+
+
+def _random_mix(seed, count, nmax, kmax, mmax):
+    rng = random.Random(seed)
+    fs = []
+    for _ in range(count):
+        n = rng.randint(1, nmax)
+        m = rng.randint(1, mmax)
+        f = []
+        for _ in range(m):
+            k = rng.randint(1, min(kmax, n))
+            f.append([v if rng.random() < 0.5 else -v for v in rng.sample(range(1, n + 1), k)])
+        if rng.random() < 0.2 and f:   # duplicate literals and tautologies, as REF.py accepts them
+            c = f[rng.randrange(len(f))]
+            if len(c) < kmax:
+                c.append(c[0] if rng.random() < 0.5 else -c[0])
+        fs.append(f)
+    return fs
+
+
+def _run_policy(batch, policy, **kw):
+    _capi.set_kernel(policy)
+    try:
+        return dpll_batch(batch, mode="sound", **kw)
+    finally:
+        _capi.set_kernel(_capi.KERNEL_AUTO)
+
+
+@pytest.mark.parametrize("seed,nmax,kmax,mmax", [(1, 12, 3, 60), (2, 20, 5, 120), (3, 600, 3, 40)])
+def test_scan_kernel_matches_general_and_oracle(seed, nmax, kmax, mmax):
+    """The clause-scan kernel (dpll_scan.hip) against the general kernel and the
+    oracle: SOUND mode, first model and full enumeration, every counter."""
+    fs = _random_mix(seed, 240, nmax, kmax, mmax)
+    for maxs, cap in ((1, 1), (0, 32)):
+        rs = _run_policy(fs, _capi.KERNEL_SCAN, max_solutions=maxs, sol_cap=cap, time_limit=20.0)
+        rg = _run_policy(fs, _capi.KERNEL_GENERAL, max_solutions=maxs, sol_cap=cap, time_limit=20.0)
+        assert (rs.status == rg.status).all()
+        assert (rs.counters[:, :7] == rg.counters[:, :7]).all()
+        assert (rs.root_len == rg.root_len).all()
+        for b, f in enumerate(fs):
+            assert rs.solutions(b) == rg.solutions(b), f
+            assert rs.root_assignment(b) == rg.root_assignment(b)
+        for b in range(0, len(fs), 7):
+            o = oracle.dpll(fs[b], "sound", max_solutions=maxs, sol_cap=cap)
+            for key in CTR:
+                assert rs.counter_dict(b)[key] == o["counters"][key], (key, fs[b])
+            assert rs.solutions(b) == o["solutions"][:cap]
+
+
+def test_scan_kernel_full_size_matches_general():
+    batch = cnf.uniform_ksat(2048, 100, 426, 3, seed=77)
+    rs = _run_policy(batch, _capi.KERNEL_SCAN, max_solutions=1, sol_cap=1)
+    rg = _run_policy(batch, _capi.KERNEL_GENERAL, max_solutions=1, sol_cap=1)
+    assert (rs.status == rg.status).all()
+    assert (rs.counters[:, :7] == rg.counters[:, :7]).all()
+    assert (rs.sol_lits == rg.sol_lits).all()
+
+
+def test_scan_policy_rejects_ineligible():
+    f = [[1, 2], [-1, 2], []]
+    _capi.set_kernel(_capi.KERNEL_SCAN)
+    try:
+        with pytest.raises(_capi.SatmiError):
+            dpll_batch([f], mode="sound", max_solutions=1)      # an empty clause
+        with pytest.raises(_capi.SatmiError):
+            dpll_batch([[[1, 2]]], mode="ref", max_solutions=0)  # REF mode
+    finally:
+        _capi.set_kernel(_capi.KERNEL_AUTO)
+
+
+def test_scan_broken_length_promise_is_too_large():
+    import torch
+    # 5-literal clauses under a promise of <= 3 (the 3-slot clause packing)
+    batch = cnf.uniform_ksat(4, 20, 60, 5, seed=5)
+    dev = torch.device("cuda", 0)
+    t = [torch.from_numpy(a).to(dev) for a in (batch.inst_clause_begin, batch.clause_lit_begin, batch.lits,
+                                             batch.inst_nvars)]
+    st = torch.zeros(4, dtype=torch.int32, device=dev)
+    ctr = torch.zeros((4, 8), dtype=torch.int64, device=dev)
+    sl = torch.zeros(4, dtype=torch.int32, device=dev)
+    so = torch.zeros((4, 20), dtype=torch.int32, device=dev)
+    L = _capi.load()
+    rc = L.satmi_dpll_batch_device(4, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), 20, 60,
+                                   300, 3, None, None, _capi.MODE_SOUND, 1, 0, 0.0, 1, 20, st.data_ptr(),
+                                   ctr.data_ptr(), sl.data_ptr(), so.data_ptr(), None, None, None)
+    _capi.check(rc, "satmi_dpll_batch_device")
+    torch.cuda.synchronize()
+    assert (st.cpu() == _capi.DPLL_TOO_LARGE).all()

@@ -25,12 +25,17 @@ def main():
     ap.add_argument("--k", type=int, default=3)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--lib", default=None, help="load this libsatmi build instead (experiments)")
+    ap.add_argument("--kernel", choices=("auto", "general", "scan"), default="auto")
     ap.add_argument("--diag", action="store_true", help="load libsatmi_diag.so and report per-phase clocks")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if a.lib:
+        _capi.LIB_PATH = os.path.abspath(a.lib)
     if a.diag:
         _capi.LIB_PATH = os.path.join(os.path.dirname(_capi.LIB_PATH), "libsatmi_diag.so")
     L = _capi.load()
+    _capi.set_kernel({"auto": _capi.KERNEL_AUTO, "general": _capi.KERNEL_GENERAL, "scan": _capi.KERNEL_SCAN}[a.kernel])
     B, n, k = a.per_gpu, a.n, a.k
     m = int(round(a.alpha * n))
     icb, clb, lits, nv = cnf.uniform_ksat_device(B, n, m, k, seed=a.seed, device=dev)
@@ -42,18 +47,14 @@ def main():
     root_len = torch.zeros(B, dtype=torch.int32, device=dev)
     root = torch.zeros((B, stride), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev)
-    lds = L.satmi_dpll_lds_bytes(n, m, m * k)
-    best = 0
-    for wpg in (4, 2, 1):
-        wgs = min(16, (160 * 1024) // (lds * wpg))
-        best = max(best, min(32, wgs * wpg)) if wgs >= 1 else best
+    kern, lds, best = _capi.plan(n, m, m * k, k)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     resident = min(B, cus * best)
     for r in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         rc = L.satmi_dpll_batch_device(B, icb.data_ptr(), clb.data_ptr(), lits.data_ptr(), nv.data_ptr(), n, m,
-                                       m * k, None, None, _capi.MODE_SOUND, 1, 0, 0.0, 1, stride, status.data_ptr(),
+                                       m * k, k, None, None, _capi.MODE_SOUND, 1, 0, 0.0, 1, stride, status.data_ptr(),
                                        ctr.data_ptr(), sl.data_ptr(), so.data_ptr(),
                                        root_len.data_ptr() if a.diag else None,
                                        root.data_ptr() if a.diag else None, st.cuda_stream)
