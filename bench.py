@@ -46,8 +46,8 @@ KERNELS = {_capi.KERNEL_SCAN: "dpll_scan_kernel", _capi.KERNEL_GENERAL: "dpll_ba
 WORKLOADS = {
     "3sat-n100": (262144, 100, 4.26, 3, 0, "configs[2]"),
     "3sat-n50": (4096, 50, 4.26, 3, 0, "configs[1]"),
-    "uf250": (4096, 250, 4.26, 3, 20000, "configs[4]"),
-    "5sat-n200": (1024, 200, 21.117, 5, 20000, "configs[4]"),
+    "uf250": (6144, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,072 resident waves
+    "5sat-n200": (1536, 200, 21.117, 5, 20000, "configs[4]"),  # 2 x the 768 resident waves
 }
 
 
