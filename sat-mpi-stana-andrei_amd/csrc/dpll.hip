@@ -44,6 +44,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -871,27 +872,35 @@ static bool make_layout(int max_vars, int max_clauses, int max_lits, DpllLayout 
     return o <= 160u * 1024u;
 }
 
+// Per-device launch state.  Each stream gets its own work counter, so batches
+// launched on different streams (a pipelined caller overlapping one batch's
+// tail with the next batch) never share a queue; launches on one stream are
+// ordered, so reusing that stream's counter is safe.
 struct DeviceWork {
-    uint32_t *counter = nullptr;
+    std::unordered_map<hipStream_t, uint32_t *> counters;
     double ticks_per_s = 1e8;
+    bool init = false;
 };
 static std::mutex g_work_mu;
 static std::vector<DeviceWork> g_work;
 static std::atomic<int> g_kernel_policy{SATMI_KERNEL_AUTO};
 
-static int device_work(DeviceWork **out) {
+static int device_work(hipStream_t stream, DeviceWork **out, uint32_t **counter) {
     int dev = 0;
     SATMI_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_work_mu);
     if ((int)g_work.size() <= dev) g_work.resize(dev + 1);
     DeviceWork &w = g_work[dev];
-    if (!w.counter) {
-        SATMI_HIP(hipMalloc(&w.counter, 256));
+    if (!w.init) {
         int khz = 0;
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
             w.ticks_per_s = (double)khz * 1000.0;
+        w.init = true;
     }
+    uint32_t *&c = w.counters[stream];
+    if (!c) SATMI_HIP(hipMalloc(&c, 256));
     *out = &w;
+    *counter = c;
     return SATMI_OK;
 }
 
@@ -989,7 +998,8 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
     }
     if (scan_ok) {
         DeviceWork *w = nullptr;
-        int rc = device_work(&w);
+        uint32_t *wc = nullptr;
+        int rc = device_work((hipStream_t)stream, &w, &wc);
         if (rc) return rc;
         int dev = 0, cus = 256;
         SATMI_HIP(hipGetDevice(&dev));
@@ -1016,10 +1026,10 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         Lc.sol_lits = d_sol_lits;
         Lc.root_len = d_root_len;
         Lc.root_lits = d_root_lits;
-        Lc.work_counter = w->counter;
+        Lc.work_counter = wc;
         Lc.num_cus = cus;
         Lc.stream = (hipStream_t)stream;
-        SATMI_HIP(hipMemsetAsync(w->counter, 0, sizeof(uint32_t), Lc.stream));
+        SATMI_HIP(hipMemsetAsync(wc, 0, sizeof(uint32_t), Lc.stream));
         return dpll_scan_launch(Lc);
     }
     DpllLayout lay;
@@ -1029,7 +1039,8 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         return SATMI_ERR_TOO_LARGE;
     }
     DeviceWork *w = nullptr;
-    int rc = device_work(&w);
+    uint32_t *wc = nullptr;
+    int rc = device_work((hipStream_t)stream, &w, &wc);
     if (rc) return rc;
     // Occupancy is set by LDS: pick the workgroup shape that keeps the most
     // waves resident (<= 32 waves and, conservatively, <= 16 workgroups per CU).
@@ -1070,11 +1081,11 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
     A.sol_lits = d_sol_lits;
     A.root_len = d_root_len;
     A.root_lits = d_root_lits;
-    A.work_counter = w->counter;
+    A.work_counter = wc;
     A.lay = lay;
 
     hipStream_t s = (hipStream_t)stream;
-    SATMI_HIP(hipMemsetAsync(w->counter, 0, sizeof(uint32_t), s));
+    SATMI_HIP(hipMemsetAsync(wc, 0, sizeof(uint32_t), s));
     if (wg_lds > 64u * 1024u)
         SATMI_HIP(hipFuncSetAttribute((const void *)dpll_batch_kernel,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)wg_lds));

@@ -250,3 +250,39 @@ def test_scan_broken_length_promise_is_too_large():
     _capi.check(rc, "satmi_dpll_batch_device")
     torch.cuda.synchronize()
     assert (st.cpu() == _capi.DPLL_TOO_LARGE).all()
+
+
+def test_concurrent_streams_keep_separate_work_queues():
+    """Two batches launched on two streams at once (bench.py's pipelined steps)
+    each draw from their own stream's work counter: results equal the
+    one-at-a-time host path."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    L = _capi.load()
+    n, m, k, B = 60, 256, 3, 2048
+    runs = []
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    for j, s in enumerate(streams):
+        icb, clb, lits, nv = cnf.uniform_ksat_device(B, n, m, k, seed=77 + j, device=dev)
+        out = (torch.zeros(B, dtype=torch.int32, device=dev),
+               torch.zeros((B, _capi.NCOUNTERS), dtype=torch.int64, device=dev),
+               torch.zeros(B, dtype=torch.int32, device=dev),
+               torch.zeros((B, n), dtype=torch.int32, device=dev))
+        runs.append(((icb, clb, lits, nv), out))
+    torch.cuda.synchronize()
+    for (batch, out), s in zip(runs, streams):
+        icb, clb, lits, nv = batch
+        st, ctr, sl, sol = out
+        rc = L.satmi_dpll_batch_device(B, icb.data_ptr(), clb.data_ptr(), lits.data_ptr(), nv.data_ptr(), n, m,
+                                       m * k, k, None, None, _capi.MODE_SOUND, 1, 0, 0.0, 1, n, st.data_ptr(),
+                                       ctr.data_ptr(), sl.data_ptr(), sol.data_ptr(), None, None, s.cuda_stream)
+        _capi.check(rc, "satmi_dpll_batch_device")
+    torch.cuda.synchronize()
+    for (batch, out) in runs:
+        host = cnf.CnfBatch(*(t.cpu().numpy() for t in batch))
+        ref = dpll_batch(host, mode="sound", max_solutions=1)
+        st, ctr, sl, sol = (t.cpu().numpy() for t in out)
+        assert (st == ref.status).all()
+        assert (ctr[:, :7] == ref.counters[:, :7]).all()
+        assert (sl == ref.sol_len[:, 0]).all()
