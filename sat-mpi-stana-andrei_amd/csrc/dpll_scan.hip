@@ -46,19 +46,44 @@
 namespace satmi {
 namespace {
 
+// Diagnostic build only (make diag): per-phase shader-clock accounting, written
+// as int64[8] over the caller's root_lits row (tools/dpll_probe.py --diag).
+#ifdef SATMI_PHASE_STAMPS
+struct PhaseClock {
+    uint64_t acc[8];
+    uint64_t t;
+    __device__ void start() {
+        for (int i = 0; i < 8; ++i) acc[i] = 0;
+        t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ void mark(int i) {
+        const uint64_t x = __builtin_amdgcn_s_memtime();
+        acc[i] += x - t;
+        t = x;
+    }
+};
+#else
+struct PhaseClock {
+    __device__ void start() {}
+    __device__ void mark(int) {}
+};
+#endif
+enum { PH_STAGE = 0, PH_ASSIGN = 1, PH_UNITS = 2, PH_CONFLICT = 3, PH_COUNTS = 4, PH_CHOOSE = 5, PH_PURE = 6,
+       PH_OTHER = 7 };
+
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr uint32_t PHASE_BIT = 0x8000u;
 
-// Literal state word lv[code] (code = v << 1 | negative).  The sum of a
-// clause's words: bits 0-2 = free occurrences (REF.py's len(c)), bits 3-7 =
-// 8 x true occurrences (!= 0: the reference dropped the clause), bits 8+ = sum
-// of the free codes (exactly one free occurrence: the unit literal).  Code 0
-// (variable 0, positive) pads short clauses and is pinned false; code 1 is
-// pinned true and fills the dummy clauses that round the clause array up to
-// whole 64-clause chunks.
-constexpr uint32_t LV_TRUE = 8u, LV_FALSE = 0u;
+// Literal state byte lv[code] (code = v << 1 | negative): free 1, true 8,
+// false 0.  The sum of a clause's bytes: bits 0-2 = free occurrences (REF.py's
+// len(c)), bits 3-7 = 8 x true occurrences (!= 0: the reference dropped the
+// clause); a unit clause's literal is its one free slot.  Code 0 (variable 0,
+// positive) pads short clauses and is pinned false; code 1 is pinned true and
+// fills the dummy clauses that round the clause array up to whole 64-clause
+// chunks.  One byte per code (not a word) packs 4 codes per LDS dword: a
+// gather of 32 random codes of n=100 touches at most 2 dwords per bank.
+constexpr uint32_t LV_TRUE = 8u, LV_FALSE = 0u, LV_FREE = 1u;
 constexpr uint32_t CODE_PAD = 0u, CODE_DUMMY = 1u;
-__device__ __forceinline__ uint32_t lv_free(uint32_t code) { return 1u + (code << 8); }
 __device__ __forceinline__ bool sum_true(uint32_t s) { return (s & 0xF8u) != 0u; }
 __device__ __forceinline__ uint32_t sum_nfree(uint32_t s) { return s & 7u; }
 
@@ -78,6 +103,11 @@ struct Pack<5> {
     static constexpr int MAXV = 2047;
     static constexpr int UNROLL = 2;
 };
+
+// Clause slots of an instance of m clauses: whole 64-clause chunks (padding a
+// partial unroll group with dummy chunks was measured slower -- the kernel is
+// LDS-throughput bound, not latency bound).
+__host__ __device__ __forceinline__ int padded_clauses(int m) { return (m + 63) & ~63; }
 
 template <int K>
 __device__ __forceinline__ uint32_t field(typename Pack<K>::W w, int j) {
@@ -104,7 +134,7 @@ struct ScanArgs {
 template <int K>
 struct SLds {
     typename Pack<K>::W *cls;   // [mcap rounded up to 64]  packed literal codes per clause
-    uint32_t *lv;               // [2(ncap+1)]  literal state words
+    uint8_t *lv;                // [2(ncap+1)]  literal state bytes
     uint32_t *ts;               // [ncap+1]  snapshot index of the assignment in the running batch
     uint32_t *cnt;              // [ncap+1]  free occurrences in active clauses, pos | neg << 16
     uint32_t *first;            // [ncap+1]  first free occurrence, position c << 3 | slot
@@ -115,16 +145,16 @@ struct SLds {
     uint32_t *plist;            // scratch:  pure-literal positions (analysis), aliases snap
 };
 
-// literal `code` becomes true: one 8-byte store sets both literals of its variable
-__device__ __forceinline__ void lv_assign(uint32_t *lv, uint32_t code) {
-    *(uint64_t *)(lv + (code & ~1u)) = (code & 1u) ? ((uint64_t)LV_TRUE << 32) : (uint64_t)LV_TRUE;
+// literal `code` becomes true: one 2-byte store sets both literals of its variable
+__device__ __forceinline__ void lv_assign(uint8_t *lv, uint32_t code) {
+    *(uint16_t *)(lv + (code & ~1u)) = (uint16_t)((code & 1u) ? (LV_TRUE << 8) : LV_TRUE);
 }
-__device__ __forceinline__ void lv_clear(uint32_t *lv, uint32_t v) {
-    *(uint64_t *)(lv + 2 * v) = (uint64_t)lv_free(2 * v) | ((uint64_t)lv_free(2 * v + 1) << 32);
+__device__ __forceinline__ void lv_clear(uint8_t *lv, uint32_t v) {
+    *(uint16_t *)(lv + 2 * v) = (uint16_t)(LV_FREE | (LV_FREE << 8));
 }
-__device__ __forceinline__ bool var_free(const uint32_t *lv, uint32_t v) { return (lv[2 * v] & 1u) != 0u; }
+__device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return (lv[2 * v] & 1u) != 0u; }
 
-// Apply f(c, w, x) to every clause c (w its packed word, x[j] the state word of
+// Apply f(c, w, x) to every clause c (w its packed word, x[j] the state byte of
 // its slot j), one 64-clause chunk per lane step; the loads of U chunks are
 // issued before any is used.  mpad is a multiple of 64 (dummy clauses are
 // always satisfied).
@@ -162,22 +192,47 @@ __device__ __forceinline__ uint32_t clause_sum(const uint32_t (&x)[K]) {
     return s;
 }
 
-// Scan for unit_propagate: the unit-clause snapshot (REF.py:143), in clause
-// order, into S.snap; *any_empty: some clause has no free literal left.
+// The literal of a unit clause: its one free slot.
 template <int K>
-__device__ int scan_units(const SLds<K> &S, int mpad, bool *any_empty) {
+__device__ __forceinline__ uint32_t unit_code(typename Pack<K>::W w, const uint32_t (&x)[K]) {
+    uint32_t code = field<K>(w, 0);
+#pragma unroll
+    for (int j = 1; j < K; ++j)
+        if (x[j] & 1u) code = field<K>(w, j);
+    return code;
+}
+
+// Snapshot stamps ts[v]: epoch << 16 | (0xFFFF - k) for the variable of
+// snapshot entry k.  Every snapshot gets a fresh epoch, so stamps never need
+// clearing: an older epoch is smaller, and atomicMax keeps the first entry of
+// a variable (the smallest k) within the current one.
+constexpr uint32_t EPOCH_LIMIT = 0xFFFFu - 4096u;   // > rounds of one propagate call (<= n+1 <= 2048)
+__device__ __forceinline__ uint32_t stamp(uint32_t ep, uint32_t k) { return (ep << 16) | (0xFFFFu - k); }
+__device__ __forceinline__ uint32_t stamp_index(uint32_t st) { return 0xFFFFu - (st & 0xFFFFu); }
+
+// Scan for unit_propagate: the unit-clause snapshot (REF.py:143), in clause
+// order, into S.snap, each entry's variable stamped with epoch `ep` (the first
+// occurrence of a variable keeps the smallest index: REF.py:149-152's
+// `if var in a`); *any_empty: some clause has no free literal left.
+template <int K>
+__device__ int scan_units(const SLds<K> &S, int mpad, uint32_t ep, bool *any_empty) {
     using W = typename Pack<K>::W;
     const uint64_t lt = lanemask_lt();
     int nu = 0;
     bool emp = false;
-    for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int, W, const uint32_t(&x)[K]) {
+    for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int c, W, const uint32_t(&x)[K]) {
         const uint32_t s = clause_sum<K>(x);
         const bool open = !sum_true(s);
         const uint32_t nf = sum_nfree(s);
         emp |= open && nf == 0u;
         const bool unit = open && nf == 1u;
         const uint64_t mk = __ballot(unit);
-        if (unit) S.snap[nu + __popcll(mk & lt)] = (uint16_t)(s >> 8);
+        if (unit) {
+            const uint32_t k = (uint32_t)nu + (uint32_t)__popcll(mk & lt);
+            const uint32_t code = unit_code<K>(S.cls[c], x);   // re-read: keeps U words out of VGPRs
+            S.snap[k] = (uint16_t)code;
+            atomicMax(&S.ts[code >> 1], stamp(ep, k));
+        }
         nu += __popcll(mk);
     });
     wave_sync();
@@ -186,20 +241,21 @@ __device__ int scan_units(const SLds<K> &S, int mpad, bool *any_empty) {
 }
 
 // The snapshot index whose assignment emptied a clause first: an emptied
-// clause was emptied by the latest-stamped of its literals (REF.py:161-162).
+// clause was emptied by the latest-stamped of its literals (REF.py:161-162);
+// `ep` is the epoch of the batch just assigned (older stamps: earlier batches).
 template <int K>
-__device__ int empty_time(const SLds<K> &S, int mpad) {
+__device__ int empty_time(const SLds<K> &S, int mpad, uint32_t ep) {
     using W = typename Pack<K>::W;
     int e = INT_MAX;
-    for_chunks<K, 1>(S, mpad, [&](int, W w, const uint32_t(&x)[K]) {
+    for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int, W w, const uint32_t(&x)[K]) {
         const uint32_t s = clause_sum<K>(x);
         if (!sum_true(s) && sum_nfree(s) == 0u) {
             int t = -1;
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const uint32_t code = field<K>(w, j);
-                const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : NONE32;
-                if (st != NONE32) t = max(t, (int)st);
+                const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : 0u;
+                if ((st >> 16) == ep) t = max(t, (int)stamp_index(st));
             }
             e = min(e, t);
         }
@@ -207,26 +263,36 @@ __device__ int empty_time(const SLds<K> &S, int mpad) {
     return wave_min_i32(e);
 }
 
-// unit_propagate (REF.py:139-165) from the snapshot S.snap[0, nu).  Returns
+// The epoch of a decision snapshot.  No stamp is live between propagate calls,
+// so this is where the 16-bit epoch wraps: all stamps are reset to epoch 0.
+template <int K>
+__device__ uint32_t next_decision_epoch(const SLds<K> &S, int n, uint32_t ep) {
+    if (ep < EPOCH_LIMIT) return ep + 1;
+    for (int v = lane_id(); v <= n; v += 64) S.ts[v] = 0u;
+    wave_sync();
+    return 1;
+}
+
+// unit_propagate (REF.py:139-165) from the snapshot S.snap[0, nu), stamped
+// with epoch `ep` (the last epoch used; each scan takes the next).  Returns
 // true on conflict; `tl` ends where the reference stops (the assignments it
 // made, including the one that emptied a clause).  `dec`: the first batch is
 // the decision literal, which REF.py's counters do not count as a propagation.
 template <int K>
-__device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec, int64_t &props,
-                          int64_t &rounds) {
+__device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec, uint32_t &ep, int64_t &props,
+                          int64_t &rounds, PhaseClock &ph) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     while (nu > 0) {
         ++rounds;
         const int rs = tl;
+        const uint32_t bep = ep;   // the batch's epoch
         for (int k0 = 0; k0 < nu; k0 += 64) {
             const int k = k0 + ln;
             const bool valid = k < nu;
             const uint32_t code = valid ? (uint32_t)S.snap[k] : 0u;
             const uint32_t v = code >> 1;
-            if (valid) atomicMin(&S.ts[v], (uint32_t)k);
-            wave_sync();
-            const bool first = valid && S.ts[v] == (uint32_t)k;
+            const bool first = valid && S.ts[v] == stamp(bep, (uint32_t)k);
             const uint64_t mk = __ballot(first);
             if (first) {
                 S.trail[tl + __popcll(mk & lt)] = (uint16_t)code;
@@ -235,33 +301,29 @@ __device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec,
             tl += __popcll(mk);
         }
         wave_sync();
+        ph.mark(PH_ASSIGN);
         const int nassign = tl - rs;
         bool emptied = false;
-        const int nu_next = scan_units<K>(S, mpad, &emptied);
+        const int nu_next = scan_units<K>(S, mpad, ++ep, &emptied);
+        ph.mark(PH_UNITS);
         if (emptied) {
             // the reference stopped at snapshot index e: keep the prefix of the
             // batch stamped <= e (the batch is in stamp order)
-            const int e = empty_time<K>(S, mpad);
+            const int e = empty_time<K>(S, mpad, bep);
             int keep = 0;
             for (int i0 = rs; i0 < tl; i0 += 64) {
                 const int i = i0 + ln;
-                const bool p = i < tl && S.ts[S.trail[i] >> 1] <= (uint32_t)e;
+                const bool p = i < tl && (int)stamp_index(S.ts[S.trail[i] >> 1]) <= e;
                 keep += __popcll(__ballot(p));
             }
             const int cut = rs + keep;
-            wave_sync();
-            for (int i = rs + ln; i < tl; i += 64) {
-                const uint32_t v = S.trail[i] >> 1;
-                S.ts[v] = NONE32;
-                if (i >= cut) lv_clear(S.lv, v);
-            }
+            for (int i = cut + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
             wave_sync();
             tl = cut;
             props += keep - (dec ? 1 : 0);
+            ph.mark(PH_CONFLICT);
             return true;
         }
-        for (int i = rs + ln; i < tl; i += 64) S.ts[S.trail[i] >> 1] = NONE32;
-        wave_sync();
         props += nassign - (dec && nassign > 0 ? 1 : 0);
         dec = false;
         if (nassign == 0) break;   // `changed` stayed False (REF.py:141-142)
@@ -384,9 +446,11 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
     using W = typename Pack<K>::W;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const int ln = lane_id();
+    PhaseClock ph;
+    ph.start();
     const int cb = A.inst_clause_begin[b], ce = A.inst_clause_begin[b + 1];
     const int m = ce - cb;
-    const int mpad = (m + 63) & ~63;
+    const int mpad = padded_clauses(m);
     const int L = A.clause_lit_begin[ce] - A.clause_lit_begin[cb];
     const int n = A.inst_nvars[b];
     int64_t *ctr = A.counters + (int64_t)b * SATMI_NCOUNTERS;
@@ -419,7 +483,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
             } else {
                 lv_clear(S.lv, (uint32_t)v);
             }
-            S.ts[v] = NONE32;
+            S.ts[v] = 0u;
             S.cnt[v] = 0u;
             S.first[v] = NONE32;
         }
@@ -433,10 +497,13 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
         return;
     }
     wave_sync();
+    ph.mark(PH_STAGE);
 
     // root snapshot: the input's unit clauses in order (no clause is empty yet)
     bool root_empty = false;
-    int nu = scan_units<K>(S, mpad, &root_empty);
+    uint32_t ep = 1;
+    int nu = scan_units<K>(S, mpad, ep, &root_empty);
+    ph.mark(PH_UNITS);
     int64_t nodes = 1, decisions = 0, props = 0, pures = 0, conflicts = 0, sols = 0, rounds = 0;
     int depth = 0, tl = 0;
     int status = SATMI_DPLL_EXHAUSTED;
@@ -446,7 +513,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
 
     while (state != ST_DONE) {
         if (state == ST_PROPAGATE) {
-            const bool conflict = propagate<K>(S, mpad, tl, nu, dec_round, props, rounds);
+            const bool conflict = propagate<K>(S, mpad, tl, nu, dec_round, ep, props, rounds, ph);
             dec_round = false;
             if (at_root) {
                 at_root = false;
@@ -464,22 +531,29 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
         if (state == ST_ANALYZE) {
             bool leaf = false;
             Choice r{0, 0u};
-            if (scan_counts<K>(S, mpad) == 0) {
+            ph.mark(PH_OTHER);
+            const int nact = scan_counts<K>(S, mpad);
+            ph.mark(PH_COUNTS);
+            if (nact == 0) {
                 leaf = true;                                   // REF.py:170-171
             } else {
                 r = choose<K>(S, n);
                 if (r.npure == 0 && r.best_var == 0u) leaf = true;   // REF.py:205-206
             }
+            ph.mark(PH_CHOOSE);
             if (!leaf && r.npure > 0) {                        // REF.py:186-195
                 tl = assign_pures<K>(S, r.npure, tl);
+                ph.mark(PH_PURE);
                 pures += r.npure;
                 ++nodes;                                       // recursive call; its unit_propagate is a no-op
             } else if (!leaf) {                                // REF.py:208-213, as formula + [[var]]
                 const uint32_t v = r.best_var;
+                ep = next_decision_epoch<K>(S, n, ep);
                 if (ln == 0) {
                     S.fvar[depth] = (uint16_t)v;
                     S.ftrail[depth] = (uint16_t)tl;
                     S.snap[0] = (uint16_t)(v << 1);            // True first
+                    S.ts[v] = stamp(ep, 0u);
                 }
                 ++depth;
                 ++decisions;
@@ -513,9 +587,11 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
                 tl = ft;
                 wave_sync();
                 if (!(fv & PHASE_BIT)) {
+                    ep = next_decision_epoch<K>(S, n, ep);
                     if (ln == 0) {
                         S.fvar[top] = (uint16_t)(fv | PHASE_BIT);
                         S.snap[0] = (uint16_t)((fv << 1) | 1u);    // False
+                        S.ts[fv] = stamp(ep, 0u);
                     }
                     ++decisions;
                     ++nodes;
@@ -538,6 +614,11 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
             }
         }
     }
+#ifdef SATMI_PHASE_STAMPS
+    ph.mark(PH_OTHER);
+    if (A.root_lits && A.sol_stride >= 16 && ln < 8)
+        ((int64_t *)(A.root_lits + (int64_t)b * A.sol_stride))[ln] = (int64_t)ph.acc[ln];
+#endif
     if (ln == 0) {
         A.status[b] = status;
         ctr[SATMI_CTR_NODES] = nodes;
@@ -559,7 +640,7 @@ __global__ void __launch_bounds__(256, SATMI_SCAN_WAVES_PER_SIMD) dpll_scan_kern
     unsigned char *base = smem + (size_t)(threadIdx.x >> 6) * A.lay.bytes;
     SLds<K> S;
     S.cls = (typename Pack<K>::W *)(base + A.lay.cls);
-    S.lv = (uint32_t *)(base + A.lay.lv);
+    S.lv = (uint8_t *)(base + A.lay.lv);
     S.ts = (uint32_t *)(base + A.lay.ts);
     S.cnt = (uint32_t *)(base + A.lay.cnt);
     S.first = (uint32_t *)(base + A.lay.first);
@@ -590,10 +671,10 @@ int pick_k(int max_vars, int max_clause_len) {
 bool make_layout(int K, int max_vars, int max_clauses, ScanLayout *lay) {
     if (max_vars < 0 || max_clauses < 0 || max_clauses > 65534) return false;
     const uint32_t N = (uint32_t)max_vars + 1, M = (uint32_t)max_clauses + 1;
-    const uint32_t Mpad = ((uint32_t)max_clauses + 63u) & ~63u;
+    const uint32_t Mpad = (uint32_t)padded_clauses(max_clauses);
     uint32_t o = 0;
     lay->cls = o;     o = align16(o + (K == 3 ? 4u : 8u) * Mpad);
-    lay->lv = o;      o = align16(o + 8 * N);
+    lay->lv = o;      o = align16(o + 2 * N);
     lay->ts = o;      o = align16(o + 4 * N);
     lay->cnt = o;     o = align16(o + 4 * N);
     lay->first = o;   o = align16(o + 4 * N);

@@ -74,7 +74,9 @@ def main():
                "wave_cycles_per_node_est": float(ticks.sum()) * tick_s * 2.1e9 / float(c[:, 0].sum()),
                "sat": int((c[:, 5] > 0).sum())}
         if a.diag:
-            names = ("stage", "assign", "apply", "collect", "analyze", "pure", "backtrack", "other")
+            names = (("stage", "assign", "units", "conflict", "counts", "choose", "pure", "other")
+                     if kern == _capi.KERNEL_SCAN else
+                     ("stage", "assign", "apply", "collect", "analyze", "pure", "backtrack", "other"))
             ph = root[:, :16].cpu().contiguous().view(torch.int64)[:, :8].double().sum(0)
             nodes = float(c[:, 0].sum())
             out["cycles_per_node"] = {nm: float(ph[i]) / nodes for i, nm in enumerate(names)}
