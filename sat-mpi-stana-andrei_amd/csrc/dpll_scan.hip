@@ -634,13 +634,23 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
 
 // Persistent grid: waves pull instance indices from a global counter until the
 // batch is drained (search-tree sizes differ by orders of magnitude).
-template <int K>
-__global__ void __launch_bounds__(256, SATMI_SCAN_WAVES_PER_SIMD) dpll_scan_kernel(ScanArgs A) {
+// LVS > 0: one-wave workgroups whose literal states live in a static LDS array
+// of LVS bytes -- its address is fixed at code generation, so a gather
+// addresses lv[code] with the code register and an immediate offset (no
+// per-wave base add per literal).  LVS = 0: multi-wave workgroups, the waves
+// taking consecutive images of the dynamic LDS, lv included.
+template <int K, int LVS>
+__global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpll_scan_kernel(ScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char *base = smem + (size_t)(threadIdx.x >> 6) * A.lay.bytes;
+    unsigned char *base = LVS ? smem : smem + (size_t)(threadIdx.x >> 6) * A.lay.bytes;
     SLds<K> S;
     S.cls = (typename Pack<K>::W *)(base + A.lay.cls);
-    S.lv = (uint8_t *)(base + A.lay.lv);
+    if constexpr (LVS > 0) {
+        __shared__ __attribute__((aligned(16))) uint8_t lv_static[LVS];
+        S.lv = lv_static;
+    } else {
+        S.lv = (uint8_t *)(base + A.lay.lv);
+    }
     S.ts = (uint32_t *)(base + A.lay.ts);
     S.cnt = (uint32_t *)(base + A.lay.cnt);
     S.first = (uint32_t *)(base + A.lay.first);
@@ -659,6 +669,14 @@ __global__ void __launch_bounds__(256, SATMI_SCAN_WAVES_PER_SIMD) dpll_scan_kern
     }
 }
 
+// Static literal-state size class of the one-wave kernel: 2(n+1) bytes rounded
+// up to 256 (n <= 127) or to the packing's variable limit.
+int lv_static_class(int K, int max_vars) {
+    const int need = 2 * (max_vars + 1);
+    if (K == 3) return need <= 256 ? 256 : 2 * (Pack<3>::MAXV + 1);
+    return 2 * (Pack<5>::MAXV + 1);
+}
+
 uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
 int pick_k(int max_vars, int max_clause_len) {
@@ -668,13 +686,13 @@ int pick_k(int max_vars, int max_clause_len) {
     return 0;
 }
 
-bool make_layout(int K, int max_vars, int max_clauses, ScanLayout *lay) {
+bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, ScanLayout *lay) {
     if (max_vars < 0 || max_clauses < 0 || max_clauses > 65534) return false;
     const uint32_t N = (uint32_t)max_vars + 1, M = (uint32_t)max_clauses + 1;
     const uint32_t Mpad = (uint32_t)padded_clauses(max_clauses);
     uint32_t o = 0;
+    lay->lv = o;      o = align16(o + (with_lv ? 2 * N : 0u));   // one-wave kernel: static LDS instead
     lay->cls = o;     o = align16(o + (K == 3 ? 4u : 8u) * Mpad);
-    lay->lv = o;      o = align16(o + 2 * N);
     lay->ts = o;      o = align16(o + 4 * N);
     lay->cnt = o;     o = align16(o + 4 * N);
     lay->first = o;   o = align16(o + 4 * N);
@@ -688,16 +706,35 @@ bool make_layout(int K, int max_vars, int max_clauses, ScanLayout *lay) {
     return o <= 160u * 1024u;
 }
 
+const void *scan_fn(int K, int lvs) {
+    if (K == 3) {
+        if (lvs == 256) return (const void *)dpll_scan_kernel<3, 256>;
+        if (lvs == 1024) return (const void *)dpll_scan_kernel<3, 1024>;
+        return (const void *)dpll_scan_kernel<3, 0>;
+    }
+    return lvs ? (const void *)dpll_scan_kernel<5, 4096> : (const void *)dpll_scan_kernel<5, 0>;
+}
+
+struct ScanPlan {
+    int waves_per_wg = 1, wg_per_cu = 1, lvs = 0;
+    ScanLayout lay;
+};
+
 // Launch shape: the workgroup size that keeps the most waves resident under
-// LDS (<= 32 waves, <= 16 workgroups per CU) and the kernel's register budget
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor).
-int scan_plan(int K, const ScanLayout &lay, int *waves_per_wg, int *wg_per_cu) {
-    const void *fn = K == 3 ? (const void *)dpll_scan_kernel<3> : (const void *)dpll_scan_kernel<5>;
+// LDS (<= 32 waves per CU) and the kernel's register budget
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor); one-wave workgroups (the
+// cheaper gather addressing) whenever they reach the same residency.
+int scan_plan(int K, int max_vars, int max_clauses, ScanPlan *P) {
     int best = 0;
-    for (int wpg : {4, 2, 1}) {
+    for (int wpg : {1, 4, 2}) {
+        const int lvs = wpg == 1 ? lv_static_class(K, max_vars) : 0;
+        ScanLayout lay;
+        if (!make_layout(K, max_vars, max_clauses, lvs == 0, &lay)) continue;
+        const void *fn = scan_fn(K, lvs);
         const uint32_t wg_lds = lay.bytes * (uint32_t)wpg;
-        int wgs = std::min(16, (int)((160u * 1024u) / wg_lds));
-        if (wgs < 1) continue;
+        const uint32_t wg_all = wg_lds + (uint32_t)lvs;
+        if (wg_all > 160u * 1024u) continue;
+        int wgs = std::min(32 / wpg, (int)((160u * 1024u) / wg_all));
         if (wg_lds > 64u * 1024u)
             SATMI_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wg_lds));
         int occ = 0;
@@ -706,8 +743,10 @@ int scan_plan(int K, const ScanLayout &lay, int *waves_per_wg, int *wg_per_cu) {
         const int waves = std::min(32, wgs * wpg);
         if (waves > best) {
             best = waves;
-            *waves_per_wg = wpg;
-            *wg_per_cu = std::max(1, std::min(wgs, 32 / wpg));
+            P->waves_per_wg = wpg;
+            P->wg_per_cu = std::max(1, std::min(wgs, 32 / wpg));
+            P->lvs = lvs;
+            P->lay = lay;
         }
     }
     if (!best) {
@@ -723,35 +762,35 @@ bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_cla
     const int K = pick_k(max_vars, max_clause_len);
     if (!K || max_lits > 65535) return false;
     ScanLayout lay;
-    if (!make_layout(K, max_vars, max_clauses, &lay)) return false;
+    if (!make_layout(K, max_vars, max_clauses, true, &lay)) return false;
     if (lds_bytes) *lds_bytes = lay.bytes;
     return true;
 }
 
 int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu) {
     const int K = pick_k(max_vars, max_clause_len);
-    ScanLayout lay;
-    if (!K || !make_layout(K, max_vars, max_clauses, &lay)) return SATMI_ERR_ARG;
-    int wpg = 1, wgc = 1;
-    const int rc = scan_plan(K, lay, &wpg, &wgc);
+    if (!K) return SATMI_ERR_ARG;
+    ScanPlan P;
+    const int rc = scan_plan(K, max_vars, max_clauses, &P);
     if (rc) return rc;
-    *waves_per_cu = wpg * wgc;
+    *waves_per_cu = P.waves_per_wg * P.wg_per_cu;
     return SATMI_OK;
 }
 
 int dpll_scan_launch(const ScanLaunch &L) {
     const int K = pick_k(L.max_vars, L.max_clause_len);
-    ScanLayout lay;
-    if (!K || !make_layout(K, L.max_vars, L.max_clauses, &lay)) {
+    ScanPlan P;
+    if (!K || !dpll_scan_eligible(L.max_vars, L.max_clauses, L.max_lits, L.max_clause_len, nullptr)) {
         set_error("dpll_scan_launch: batch shape not eligible for the scan kernel");
         return SATMI_ERR_ARG;
     }
-    int waves_per_wg = 1, wg_per_cu = 1;
-    const int prc = scan_plan(K, lay, &waves_per_wg, &wg_per_cu);
+    const int prc = scan_plan(K, L.max_vars, L.max_clauses, &P);
     if (prc) return prc;
+    const ScanLayout &lay = P.lay;
+    const int waves_per_wg = P.waves_per_wg;
     const uint32_t wg_lds = lay.bytes * (uint32_t)waves_per_wg;
     const int need = (L.num_instances + waves_per_wg - 1) / waves_per_wg;
-    const int grid = std::max(1, std::min(need, L.num_cus * wg_per_cu));
+    const int grid = std::max(1, std::min(need, L.num_cus * P.wg_per_cu));
 
     ScanArgs A;
     A.inst_clause_begin = L.inst_clause_begin;
@@ -772,10 +811,17 @@ int dpll_scan_launch(const ScanLaunch &L) {
     A.root_lits = L.root_lits;
     A.work_counter = L.work_counter;
     A.lay = lay;
-    if (K == 3)
-        hipLaunchKernelGGL(dpll_scan_kernel<3>, dim3(grid), dim3(64 * waves_per_wg), wg_lds, L.stream, A);
+    const dim3 g(grid), blk(64 * waves_per_wg);
+    if (K == 3 && P.lvs == 256)
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 256>), g, blk, wg_lds, L.stream, A);
+    else if (K == 3 && P.lvs == 1024)
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 1024>), g, blk, wg_lds, L.stream, A);
+    else if (K == 3)
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 0>), g, blk, wg_lds, L.stream, A);
+    else if (P.lvs)
+        hipLaunchKernelGGL((dpll_scan_kernel<5, 4096>), g, blk, wg_lds, L.stream, A);
     else
-        hipLaunchKernelGGL(dpll_scan_kernel<5>, dim3(grid), dim3(64 * waves_per_wg), wg_lds, L.stream, A);
+        hipLaunchKernelGGL((dpll_scan_kernel<5, 0>), g, blk, wg_lds, L.stream, A);
     SATMI_HIP(hipGetLastError());
     return SATMI_OK;
 }
