@@ -149,6 +149,14 @@ int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_li
                   int trace_cap, int32_t *h_steps, int32_t *h_rec_lits, int64_t rec_lit_cap,
                   int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_step_off, int rec_step_cap);
 
+/* Device-side span of the last DPLL launch on `stream`: enqueues (on that
+ * stream, after the launch) a copy of two uint64 s_memrealtime ticks into
+ * d_span: [0] = ~(first wave's start), [1] = last wave's end, so the launch
+ * took (d_span[1] - ~d_span[0]) / satmi_wallclock_hz() seconds -- the kernel's
+ * own duration even when launches on two streams overlap. */
+int satmi_dpll_launch_span(void *stream, uint64_t *d_span);
+int satmi_wallclock_hz(double *hz);
+
 /* LDS bytes one wavefront needs for an instance of this size (0 = unsupported). */
 uint64_t satmi_dpll_lds_bytes(int max_vars, int max_clauses, int max_lits);
 

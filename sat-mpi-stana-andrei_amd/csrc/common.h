@@ -29,6 +29,17 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// Launch span of a persistent DPLL grid, kept beside its work counter
+// (work[0] = counter, work_span = (uint64_t *)work + 1): span[0] = ~(earliest
+// wave start), span[1] = latest wave end, both s_memrealtime ticks (the
+// constant wall clock); zeroed with the counter before each launch.
+__device__ __forceinline__ void span_begin(uint32_t *work) {
+    if (lane_id() == 0) atomicMax((unsigned long long *)work + 1, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void span_end(uint32_t *work) {
+    if (lane_id() == 0) atomicMax((unsigned long long *)work + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 // Order LDS traffic between lanes of the same wave (the wave executes in
 // order; this stops the compiler from caching/reordering across it).
 __device__ __forceinline__ void wave_sync() {

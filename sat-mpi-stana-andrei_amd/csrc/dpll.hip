@@ -831,6 +831,7 @@ __global__ void __launch_bounds__(256) dpll_batch_kernel(DpllArgs A) {
     S.ubits = (uint64_t *)(base + A.lay.ubits);
     S.posbits = (uint64_t *)(base + A.lay.posbits);
     S.mark = (int32_t *)(base + A.lay.mark);
+    span_begin(A.work_counter);
     for (;;) {
         uint32_t b = 0;
         if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
@@ -839,6 +840,7 @@ __global__ void __launch_bounds__(256) dpll_batch_kernel(DpllArgs A) {
         solve_instance(A, S, (int)b);
         wave_sync();
     }
+    span_end(A.work_counter);
 }
 
 // ------------------------------------------------------------------ host side
@@ -907,6 +909,33 @@ static int device_work(hipStream_t stream, DeviceWork **out, uint32_t **counter)
 }  // namespace satmi
 
 using namespace satmi;
+
+extern "C" int satmi_dpll_launch_span(void *stream, uint64_t *d_span) {
+    if (!d_span) {
+        set_error("satmi_dpll_launch_span: d_span is NULL");
+        return SATMI_ERR_ARG;
+    }
+    DeviceWork *w = nullptr;
+    uint32_t *wc = nullptr;
+    int rc = device_work((hipStream_t)stream, &w, &wc);
+    if (rc) return rc;
+    SATMI_HIP(hipMemcpyAsync(d_span, (uint64_t *)wc + 1, 2 * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                             (hipStream_t)stream));
+    return SATMI_OK;
+}
+
+extern "C" int satmi_wallclock_hz(double *hz) {
+    if (!hz) {
+        set_error("satmi_wallclock_hz: hz is NULL");
+        return SATMI_ERR_ARG;
+    }
+    DeviceWork *w = nullptr;
+    uint32_t *wc = nullptr;
+    int rc = device_work(nullptr, &w, &wc);
+    if (rc) return rc;
+    *hz = w->ticks_per_s;
+    return SATMI_OK;
+}
 
 extern "C" int satmi_dpll_set_kernel(int policy) {
     if (policy != SATMI_KERNEL_AUTO && policy != SATMI_KERNEL_GENERAL && policy != SATMI_KERNEL_SCAN) {
@@ -1029,7 +1058,7 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         Lc.work_counter = wc;
         Lc.num_cus = cus;
         Lc.stream = (hipStream_t)stream;
-        SATMI_HIP(hipMemsetAsync(wc, 0, sizeof(uint32_t), Lc.stream));
+        SATMI_HIP(hipMemsetAsync(wc, 0, 24, Lc.stream));   // counter + launch span (common.h)
         return dpll_scan_launch(Lc);
     }
     DpllLayout lay;
@@ -1085,7 +1114,7 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
     A.lay = lay;
 
     hipStream_t s = (hipStream_t)stream;
-    SATMI_HIP(hipMemsetAsync(wc, 0, sizeof(uint32_t), s));
+    SATMI_HIP(hipMemsetAsync(wc, 0, 24, s));   // counter + launch span (common.h)
     if (wg_lds > 64u * 1024u)
         SATMI_HIP(hipFuncSetAttribute((const void *)dpll_batch_kernel,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)wg_lds));

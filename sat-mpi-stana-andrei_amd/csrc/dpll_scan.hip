@@ -659,6 +659,7 @@ __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpl
     S.ftrail = (uint16_t *)(base + A.lay.ftrail);
     S.snap = (uint16_t *)(base + A.lay.scratch);
     S.plist = (uint32_t *)(base + A.lay.scratch);
+    span_begin(A.work_counter);
     for (;;) {
         uint32_t b = 0;
         if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
@@ -667,6 +668,7 @@ __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpl
         solve_instance<K>(A, S, (int)b);
         wave_sync();
     }
+    span_end(A.work_counter);
 }
 
 // Static literal-state size class of the one-wave kernel: 2(n+1) bytes rounded

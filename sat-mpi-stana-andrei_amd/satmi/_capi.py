@@ -28,6 +28,7 @@ EXPORTED = (
     "satmi_malloc", "satmi_free", "satmi_memcpy_h2d", "satmi_memcpy_d2h", "satmi_stream_synchronize",
     "satmi_dpll_batch_device", "satmi_dpll_batch_host", "satmi_dpll_lds_bytes", "satmi_resolution_host",
     "satmi_dp_host", "satmi_dpll_scan_lds_bytes", "satmi_dpll_set_kernel", "satmi_dpll_plan",
+    "satmi_dpll_launch_span", "satmi_wallclock_hz",
 )
 
 
@@ -74,6 +75,8 @@ def load():
     L.satmi_dpll_scan_lds_bytes.restype = ctypes.c_uint64
     L.satmi_dpll_scan_lds_bytes.argtypes = [ctypes.c_int] * 4
     L.satmi_dpll_set_kernel.argtypes = [ctypes.c_int]
+    L.satmi_dpll_launch_span.argtypes = [vp, vp]
+    L.satmi_wallclock_hz.argtypes = [P(ctypes.c_double)]
     L.satmi_dpll_plan.argtypes = [ctypes.c_int] * 6 + [P(ctypes.c_int), P(ctypes.c_uint64), P(ctypes.c_int)]
     L.satmi_dpll_batch_device.argtypes = [
         ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
@@ -93,6 +96,13 @@ def load():
         getattr(L, name)  # AttributeError here = library/header mismatch
     _lib = L
     return L
+
+
+def wallclock_hz():
+    """Rate of the device wall clock (s_memrealtime) that satmi_dpll_launch_span reports in."""
+    hz = ctypes.c_double(0.0)
+    check(load().satmi_wallclock_hz(ctypes.byref(hz)), "satmi_wallclock_hz")
+    return hz.value
 
 
 def plan(max_vars, max_clauses, max_lits, max_clause_len, mode=MODE_SOUND, has_init=False):
