@@ -213,18 +213,31 @@ __device__ __forceinline__ uint32_t stamp_index(uint32_t st) { return 0xFFFFu - 
 // Scan for unit_propagate: the unit-clause snapshot (REF.py:143), in clause
 // order, into S.snap, each entry's variable stamped with epoch `ep` (the first
 // occurrence of a variable keeps the smallest index: REF.py:149-152's
-// `if var in a`); *any_empty: some clause has no free literal left.
+// `if var in a`).  *empty_at: INT_MAX if no clause is empty, else the snapshot
+// index (within the batch of epoch `bep` just assigned) whose assignment
+// emptied a clause first -- an emptied clause was emptied by the
+// latest-stamped of its literals (REF.py:161-162), found in the same pass.
 template <int K>
-__device__ int scan_units(const SLds<K> &S, int mpad, uint32_t ep, bool *any_empty) {
+__device__ int scan_units(const SLds<K> &S, int mpad, uint32_t ep, uint32_t bep, int *empty_at) {
     using W = typename Pack<K>::W;
     const uint64_t lt = lanemask_lt();
     int nu = 0;
-    bool emp = false;
+    int e = INT_MAX;
     for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int c, W, const uint32_t(&x)[K]) {
         const uint32_t s = clause_sum<K>(x);
         const bool open = !sum_true(s);
         const uint32_t nf = sum_nfree(s);
-        emp |= open && nf == 0u;
+        if (open && nf == 0u) {   // rare: only in a conflicting round
+            const W w = S.cls[c];
+            int t = -1;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint32_t code = field<K>(w, j);
+                const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : 0u;
+                if ((st >> 16) == bep) t = max(t, (int)stamp_index(st));
+            }
+            e = min(e, t);
+        }
         const bool unit = open && nf == 1u;
         const uint64_t mk = __ballot(unit);
         if (unit) {
@@ -236,31 +249,8 @@ __device__ int scan_units(const SLds<K> &S, int mpad, uint32_t ep, bool *any_emp
         nu += __popcll(mk);
     });
     wave_sync();
-    *any_empty = __ballot(emp) != 0ull;
+    *empty_at = __ballot(e != INT_MAX) ? wave_min_i32(e) : INT_MAX;
     return nu;
-}
-
-// The snapshot index whose assignment emptied a clause first: an emptied
-// clause was emptied by the latest-stamped of its literals (REF.py:161-162);
-// `ep` is the epoch of the batch just assigned (older stamps: earlier batches).
-template <int K>
-__device__ int empty_time(const SLds<K> &S, int mpad, uint32_t ep) {
-    using W = typename Pack<K>::W;
-    int e = INT_MAX;
-    for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int, W w, const uint32_t(&x)[K]) {
-        const uint32_t s = clause_sum<K>(x);
-        if (!sum_true(s) && sum_nfree(s) == 0u) {
-            int t = -1;
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const uint32_t code = field<K>(w, j);
-                const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : 0u;
-                if ((st >> 16) == ep) t = max(t, (int)stamp_index(st));
-            }
-            e = min(e, t);
-        }
-    });
-    return wave_min_i32(e);
 }
 
 // The epoch of a decision snapshot.  No stamp is live between propagate calls,
@@ -303,13 +293,12 @@ __device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec,
         wave_sync();
         ph.mark(PH_ASSIGN);
         const int nassign = tl - rs;
-        bool emptied = false;
-        const int nu_next = scan_units<K>(S, mpad, ++ep, &emptied);
+        int e = INT_MAX;
+        const int nu_next = scan_units<K>(S, mpad, ++ep, bep, &e);
         ph.mark(PH_UNITS);
-        if (emptied) {
+        if (e != INT_MAX) {
             // the reference stopped at snapshot index e: keep the prefix of the
             // batch stamped <= e (the batch is in stamp order)
-            const int e = empty_time<K>(S, mpad, bep);
             int keep = 0;
             for (int i0 = rs; i0 < tl; i0 += 64) {
                 const int i = i0 + ln;
@@ -500,9 +489,9 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
     ph.mark(PH_STAGE);
 
     // root snapshot: the input's unit clauses in order (no clause is empty yet)
-    bool root_empty = false;
+    int root_empty = INT_MAX;   // no clause is empty before any assignment
     uint32_t ep = 1;
-    int nu = scan_units<K>(S, mpad, ep, &root_empty);
+    int nu = scan_units<K>(S, mpad, ep, 0u, &root_empty);
     ph.mark(PH_UNITS);
     int64_t nodes = 1, decisions = 0, props = 0, pures = 0, conflicts = 0, sols = 0, rounds = 0;
     int depth = 0, tl = 0;
