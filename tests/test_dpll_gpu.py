@@ -286,3 +286,23 @@ def test_concurrent_streams_keep_separate_work_queues():
         assert (st == ref.status).all()
         assert (ctr[:, :7] == ref.counters[:, :7]).all()
         assert (sl == ref.sol_len[:, 0]).all()
+
+
+def test_snapshot_epoch_wraparound_parity():
+    """The scan kernel tags unit-snapshot stamps with a 16-bit epoch (one per
+    snapshot) and resets every stamp when the epoch nears its limit
+    (dpll_scan.hip, next_decision_epoch).  A uf250-shaped search of 20,000
+    calls uses > 65,536 epochs, so the reset runs, and every counter and the
+    model must still equal the oracle's."""
+    n, m, k, cap = 250, 1065, 3, 20000
+    batch = cnf.uniform_ksat(2, n, m, k, seed=2026)
+    r = dpll_batch(batch, mode="sound", max_solutions=1, node_limit=cap, sol_cap=1)
+    epochs = [int(r.counters[b, 6] + r.counters[b, 1]) for b in range(2)]   # rounds + decisions
+    assert max(epochs) > 65536, epochs
+    for b in range(2):
+        o = oracle.dpll(batch.instance(b), "sound", max_solutions=1, node_limit=cap, sol_cap=1)
+        assert int(r.status[b]) == o["status"], b
+        got = r.counter_dict(b)
+        for key in CTR:
+            assert got[key] == o["counters"][key], (b, key)
+        assert r.solutions(b)[:1] == o["solutions"][:1]
