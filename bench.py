@@ -21,6 +21,12 @@ with the same harness; the default line is configs[2]):
                node-capped search (--node-limit, default 20,000 calls/instance)
     5sat-n200  configs[4]: random 5-SAT n=200 at the 5-SAT threshold
                (alpha=21.117, m=4,223): long clauses, 1 wave per CU of LDS
+    php-dp     configs[3]: Davis-Putnam elimination of pigeonhole PHP(6,5)
+               (30 variables, 81 clauses; every step's resolvents, tautology
+               and subsumption filter on the GPU) -- solves/s
+    php-res    configs[3]: resolution saturation of PHP(4,3) (pair kernel +
+               sort dedup), its first 4 passes (171,392 derived clauses; the
+               5th pass would resolve 1.5e10 pairs) -- derived clauses/s
 For the node-capped workloads the headline value is unit-props/s.
 
 Prints ONE JSON line on rank 0.
@@ -52,6 +58,8 @@ WORKLOADS = {
     "uf250": (6144, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,072 resident waves
     "5sat-n200": (1536, 200, 21.117, 5, 20000, "configs[4]"),  # 2 x the 768 resident waves
 }
+# configs[3] presets: (holes, clause_limit) -- one formula per step, host-array C ABI
+SATURATION = {"php-dp": (5, 0), "php-res": (3, 4)}   # (holes, resolution passes)
 
 
 def parse():
@@ -59,7 +67,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=sorted(WORKLOADS), default="3sat-n100")
+    p.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(SATURATION), default="3sat-n100")
     p.add_argument("--total", type=int, default=None, help="instances per step, all ranks")
     p.add_argument("--n", type=int, default=None)
     p.add_argument("--alpha", type=float, default=None)
@@ -70,6 +78,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-steps", action="store_true", help="no warmup/cpu leg (for rocprofv3 runs)")
     a = p.parse_args()
+    if a.workload in SATURATION:
+        return a
     total, n, alpha, k, node_limit, a.config_name = WORKLOADS[a.workload]
     a.total = total if a.total is None else a.total
     a.n = n if a.n is None else a.n
@@ -114,8 +124,81 @@ def load_pmc(workload_key):
         return None
 
 
+def saturation_main(args):
+    """configs[3]: Davis-Putnam / resolution saturation of a pigeonhole formula.
+    A step = one full satmi_dp_host / satmi_resolution_host call (host arrays in,
+    verdict out: the boundary these solvers have, REF.py:63-130).  Each rank
+    solves its own replica (one formula does not shard)."""
+    from satmi.dp import eliminate
+    from satmi.resolution import resolve
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    holes, npass = SATURATION[args.workload]
+    f = cnf.pigeonhole(holes)
+    if args.workload == "php-dp":
+        run = lambda: eliminate(f)                                  # noqa: E731
+        work = lambda r: 1                                          # noqa: E731
+        unit, metric_desc = "solves/s", f"Davis-Putnam elimination of PHP({holes + 1},{holes})"
+    else:
+        run = lambda: resolve(f, max_passes=npass)                  # noqa: E731
+        work = lambda r: sum(r["pass_new"])                         # noqa: E731
+        unit, metric_desc = "derived clauses/s", f"resolution saturation of PHP({holes + 1},{holes}), first {npass} passes"
+    for _ in range(0 if args.profile_steps else args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    done = 0
+    last = None
+    for _ in range(args.steps):
+        last = run()
+        done += work(last)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    out = {"metric": METRIC, "value": done * world / elapsed, "unit": unit, "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic: pigeonhole formula",
+           "config": {"workload": metric_desc + " (BASELINE configs[3]); replicas across ranks",
+                      "preset": args.workload, "parallelism": f"replicas x{world}"},
+           "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
+           # a chain of small dependent kernels per step (pair / sort / merge, or split /
+           # resolve / subsume): no single dominant kernel; rocprofv3 per-kernel stats in profiles/
+           "roofline": None}
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and not args.profile_steps:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+            t = time.perf_counter()
+            r = oracle.dp(f) if args.workload == "php-dp" else oracle.resolution(f, max_passes=npass)
+            dt = time.perf_counter() - t
+            w = 1 if args.workload == "php-dp" else sum(r["pass_new"])
+            if r["result"] != last["result"] or w != work(last):
+                raise SystemExit("bench: GPU and oracle disagree on the configs[3] workload")
+            cpu = {"value": w / dt, "unit": unit, "cores": 1, "kind": "port",
+                   "sample": f"one {metric_desc} by the oracle (oracle/*.c), single thread, {dt:.2f} s"}
+        out["cpu_baseline"] = cpu
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload in SATURATION:
+        return saturation_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <string>
 #include <vector>
 
 #include "common.h"
@@ -320,6 +321,18 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
         const int64_t ncand = (int64_t)hc.count;
         int64_t nnew = 0;
         if (ncand > 0) {
+            // the pass's working set: candidate keys + four int64 arrays of the
+            // sort/dedup; refuse (SATMI_ERR_NOMEM) rather than oversubscribe HBM
+            const double need = (double)ncand * (8.0 * K + 32.0) + 8.0 * (double)(nseen + ncand) * K;
+            size_t free_b = 0, total_b = 0;
+            SATMI_HIP(hipMemGetInfo(&free_b, &total_b));
+            if (need > 0.8 * (double)free_b) {
+                set_error("satmi_resolution_host: pass " + std::to_string(passes + 1) + " has " +
+                          std::to_string(ncand) + " candidate resolvents, needing " +
+                          std::to_string(need / 1e9) + " GB of device memory (" + std::to_string(free_b / 1e9) +
+                          " GB free); set clause_limit / max_passes");
+                return SATMI_ERR_NOMEM;
+            }
             SATMI_TRY(cand.reserve(8 * (size_t)ncand * K));
             SATMI_HIP(hipMemsetAsync(counters.p, 0, 16, s));
             hipLaunchKernelGGL(res_pairs_kernel<true>, dim3(grid), dim3(256), 0, s, clauses.as<uint64_t>(), W, jlo,

@@ -58,3 +58,13 @@ def test_pigeonhole_and_limits():
     r = resolve(cnf.uniform_ksat(1, 8, 20, 3, seed=3).instance(0), max_passes=1)
     o = oracle.resolution(cnf.uniform_ksat(1, 8, 20, 3, seed=3).instance(0), max_passes=1)
     assert r["passes"] <= 1 and r["pass_new"][:1] == o["pass_new"][:1]
+
+
+def test_pigeonhole_php43_four_passes():
+    """A mid-size saturation (bench.py --workload php-res): the first four
+    passes of PHP(4,3) -- the 4th resolves 27.8 M pairs and adds 163,954
+    clauses -- add exactly the oracle's clause counts."""
+    f = cnf.pigeonhole(3)
+    r = resolve(f, max_passes=4)
+    assert r["result"] == -1 and r["passes"] == 4
+    assert r["pass_new"] == [36, 270, 7132, 163954]
