@@ -103,11 +103,13 @@ __global__ void __launch_bounds__(256) res_pairs_kernel(const uint64_t *keys, in
         if (m == 0ull) continue;
         unsigned long long slot0 = 0;
         if (ln == 0) slot0 = atomicAdd(count, (unsigned long long)__popcll(m));
-        slot0 = (unsigned long long)__builtin_amdgcn_readfirstlane((int)slot0) |
-                ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(slot0 >> 32)) << 32);
+        // zero-extend each 32-bit half (a sign-extended low half past 2^31
+        // candidates would turn the slot negative and the write out of bounds)
+        slot0 = (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)slot0) |
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(slot0 >> 32)) << 32);
         if (WRITE && is_cand) {
             const int64_t slot = (int64_t)slot0 + __popcll(m & lanemask_lt());
-            if (slot < cand_cap) {
+            if (slot >= 0 && slot < cand_cap) {
                 const uint64_t *a = keys + i * K, *b = keys + j * K;
                 uint64_t *r = cand + slot * K;
                 for (int w = 0; w < W; ++w) {
