@@ -963,8 +963,9 @@ extern "C" int satmi_dpll_plan(int max_vars, int max_clauses, int max_lits, int 
     if (mode == SATMI_MODE_SOUND && !has_init && policy != SATMI_KERNEL_GENERAL &&
         dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, &sb)) {
         *kernel = SATMI_KERNEL_SCAN;
+        const int rc = dpll_scan_resident(max_vars, max_clauses, max_clause_len, waves_per_cu, &sb);
         *lds_bytes_per_wave = sb;
-        return dpll_scan_resident(max_vars, max_clauses, max_clause_len, waves_per_cu);
+        return rc;
     }
     DpllLayout lay;
     if (!make_layout(max_vars, max_clauses, max_lits, &lay)) {

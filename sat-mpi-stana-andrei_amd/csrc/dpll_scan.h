@@ -25,8 +25,10 @@ struct ScanLaunch {
 // assignment)?  Fills *lds_bytes with the per-wave LDS it would use.
 bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_clause_len, uint32_t *lds_bytes);
 
-// Waves of the scan kernel resident per CU for this shape (LDS and registers).
-int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu);
+// Waves of the scan kernel resident per CU for this shape (LDS and registers),
+// and the LDS bytes per wave of that launch (dynamic image + static literal states).
+int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu,
+                       uint32_t *lds_per_wave = nullptr);
 
 // Launch on L.stream (asynchronous).  The caller has checked eligibility and
 // zeroed *L.work_counter on the stream.

@@ -758,13 +758,15 @@ bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_cla
     return true;
 }
 
-int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu) {
+int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu,
+                       uint32_t *lds_per_wave) {
     const int K = pick_k(max_vars, max_clause_len);
     if (!K) return SATMI_ERR_ARG;
     ScanPlan P;
     const int rc = scan_plan(K, max_vars, max_clauses, &P);
     if (rc) return rc;
     *waves_per_cu = P.waves_per_wg * P.wg_per_cu;
+    if (lds_per_wave) *lds_per_wave = P.lay.bytes + (uint32_t)P.lvs;
     return SATMI_OK;
 }
 
