@@ -56,7 +56,9 @@ def test_scan_kernel_eligibility_query():
     assert _capi.plan(100, 426, 1278, 3, _capi.MODE_REF)[0] == _capi.KERNEL_GENERAL
     assert _capi.plan(100, 426, 1278, 3, _capi.MODE_SOUND, has_init=True)[0] == _capi.KERNEL_GENERAL
     kern, lds, _ = _capi.plan(100, 426, 1278, 3)
-    assert (kern, lds) == (_capi.KERNEL_SCAN, s100)
+    # the launch's real per-wave LDS: one-wave workgroups keep the literal states
+    # in a 256-B static array instead of the image's 2(n+1) = 202 B (+ alignment)
+    assert kern == _capi.KERNEL_SCAN and s100 - 208 + 256 == lds
     _capi.set_kernel(_capi.KERNEL_GENERAL)
     try:
         assert _capi.plan(100, 426, 1278, 3)[0] == _capi.KERNEL_GENERAL
