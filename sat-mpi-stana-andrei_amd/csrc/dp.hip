@@ -219,15 +219,28 @@ __device__ __forceinline__ bool bits_subset(const uint64_t *a, const uint64_t *b
     return true;
 }
 
-// unique_new (REF.py:122-125): kept[k] iff no rem clause and no earlier new clause is a subset
-__global__ void dp_subsume_kernel(ClauseList L, const int64_t *rlist, int64_t nrem, const uint64_t *rbits,
-                                  const int64_t *ntlist, int64_t m, int K, int64_t *kept) {
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+// unique_new (REF.py:122-125): kept[k] iff no rem clause and no earlier new
+// clause is a subset.  One wavefront per new clause: its 64 lanes test 64
+// candidate subsets per step and the wave stops at the first hit (ballot), so
+// the O(m (nrem + m)) tests spread over every wave slot of the chip instead of
+// one serial loop per thread.
+__global__ void __launch_bounds__(256) dp_subsume_kernel(ClauseList L, const int64_t *rlist, int64_t nrem,
+                                                         const uint64_t *rbits, const int64_t *ntlist, int64_t m,
+                                                         int K, int64_t *kept) {
+    const int ln = lane_id();
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; k < m; k += nwaves) {
         const uint64_t *x = rbits + ntlist[k] * K;
         bool sub = false;
-        for (int64_t e = 0; e < nrem && !sub; ++e) sub = bits_subset(L.bits + rlist[e] * K, x, K);
-        for (int64_t e = 0; e < k && !sub; ++e) sub = bits_subset(rbits + ntlist[e] * K, x, K);
-        kept[k] = !sub;
+        for (int64_t e0 = 0; e0 < nrem && !sub; e0 += 64) {
+            const int64_t e = e0 + ln;
+            sub = __ballot(e < nrem && bits_subset(L.bits + rlist[e] * K, x, K)) != 0ull;
+        }
+        for (int64_t e0 = 0; e0 < k && !sub; e0 += 64) {
+            const int64_t e = e0 + ln;
+            sub = __ballot(e < k && bits_subset(rbits + ntlist[e] * K, x, K)) != 0ull;
+        }
+        if (ln == 0) kept[k] = !sub;
     }
 }
 
@@ -544,7 +557,7 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         int64_t nkept = 0;
         if (m > 0) {
             DP_TRY(kept.need(8 * (size_t)m));
-            hipLaunchKernelGGL(dp_subsume_kernel, dim3(grid_for(m)), dim3(PRIM_BLOCK), 0, s, Lc,
+            hipLaunchKernelGGL(dp_subsume_kernel, dim3(grid_for(m * 64)), dim3(PRIM_BLOCK), 0, s, Lc,
                                rlist.as<int64_t>(), nr, rbits.as<uint64_t>(), ntlist.as<int64_t>(), m, K,
                                kept.as<int64_t>());
             SATMI_HIP(hipGetLastError());
