@@ -5,23 +5,23 @@
 // applied as a unit clause -- in a formulation built for the CDNA4 issue model
 // instead of for minimal work:
 //
-//   * The only mutable state of the formula is one word per literal code,
-//     lv[code] (free / true / false, see LV_*).  There is no per-clause state:
+//   * The only mutable state of the formula is one byte per literal code,
+//     lv[code] (free / true / false, see LV_*); four codes per LDS dword.  No clause state:
 //     the reference's reduced formula (its filtered Python lists) is
 //     *re-derived* by scanning the packed clauses, 64 clauses per wave step.
 //     A clause is one LDS word (<= 3 literal codes of 10 bits, or <= 5 of 12
-//     bits); the SUM of its literals' state words is the reduced clause:
-//     satisfied or not, its length, and (length 1) its unit literal.
+//     bits); the SUM of its literals' state bytes is the reduced clause:
+//     satisfied or not and its length (length 1: the free slot is the unit).
 //   * unit_propagate (REF.py:139-165): a scan collects the unit clauses in
 //     clause order (ballot + popcount compaction) -- exactly REF.py:143's
 //     snapshot.  The snapshot is assigned at once, the first occurrence of a
-//     variable winning (LDS atomicMin of the snapshot index: the `if var in a`
-//     rule of REF.py:149-152).  The next scan builds the next snapshot and
-//     sees emptied clauses; an emptied clause was emptied by the
+//     variable winning (epoch-tagged LDS atomicMax stamps written by the scan
+//     itself: the `if var in a` rule of REF.py:149-152).  The next scan builds
+//     the next snapshot and sees emptied clauses; an emptied clause was emptied by the
 //     latest-stamped of its literals, so the reference's stopping unit is the
 //     minimum of those stamps, and the assignments stamped after it are
 //     dropped -- counters match the reference one for one.
-//   * Backtracking clears the state words of the popped trail entries and
+//   * Backtracking clears the state bytes of the popped trail entries and
 //     nothing else: there is no clause state to undo.
 //   * Pure literals / branching (REF.py:174-208): one scan adds every free
 //     occurrence of an active clause into per-variable counters and keeps the
@@ -29,7 +29,7 @@
 //
 // A scan step is K independent LDS gathers and K-1 adds per lane, so the
 // kernel is VALU/LDS-issue bound with short dependency chains, and the
-// per-wave LDS image is small (n=100, m=426: 5.3 KB).
+// per-wave LDS image is small (n=100, m=426: 4.8 KB, 32 waves per CU).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
