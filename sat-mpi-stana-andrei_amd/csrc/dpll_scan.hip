@@ -40,7 +40,7 @@
 
 // minimum waves per SIMD the register allocation must allow (launch bounds)
 #ifndef SATMI_SCAN_WAVES_PER_SIMD
-#define SATMI_SCAN_WAVES_PER_SIMD 7
+#define SATMI_SCAN_WAVES_PER_SIMD 8
 #endif
 
 namespace satmi {
@@ -94,7 +94,7 @@ struct Pack<3> {
     using W = uint32_t;
     static constexpr int BITS = 10;
     static constexpr int MAXV = 511;
-    static constexpr int UNROLL = 4;
+    static constexpr int UNROLL = 7;
 };
 template <>
 struct Pack<5> {
@@ -159,22 +159,31 @@ __device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return
 // issued before any is used.  mpad is a multiple of 64 (dummy clauses are
 // always satisfied).
 template <int K, int U, typename F>
+__device__ __forceinline__ void chunk_group(const SLds<K> &S, int c0, F &&f) {
+    using W = typename Pack<K>::W;
+    const int ln = lane_id();
+    W w[U];
+    uint32_t x[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = S.cls[c0 + 64 * u + ln];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[u][j] = S.lv[field<K>(w[u], j)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) f(c0 + 64 * u + ln, w[u], x[u]);
+}
+
+// Groups of U chunks, then (U > 4) groups of 4, then single chunks: n=100's 7
+// chunks are one group of 7, n=50's 4 chunks one group of 4.
+template <int K, int U, typename F>
 __device__ __forceinline__ void for_chunks(const SLds<K> &S, int mpad, F &&f) {
     using W = typename Pack<K>::W;
     const int ln = lane_id();
     int c0 = 0;
-    for (; c0 + 64 * U <= mpad; c0 += 64 * U) {
-        W w[U];
-        uint32_t x[U][K];
-#pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = S.cls[c0 + 64 * u + ln];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int j = 0; j < K; ++j) x[u][j] = S.lv[field<K>(w[u], j)];
-#pragma unroll
-        for (int u = 0; u < U; ++u) f(c0 + 64 * u + ln, w[u], x[u]);
-    }
+    for (; c0 + 64 * U <= mpad; c0 += 64 * U) chunk_group<K, U>(S, c0, f);
+    if constexpr (U > 4)
+        for (; c0 + 64 * 4 <= mpad; c0 += 64 * 4) chunk_group<K, 4>(S, c0, f);
     for (; c0 < mpad; c0 += 64) {
         const W w = S.cls[c0 + ln];
         uint32_t x[K];
