@@ -89,9 +89,23 @@ def parse():
     return a
 
 
+def host_cores():
+    """CPU cores this job may use: the box's share (OMP_NUM_THREADS is set to it
+    on the GPU box; os.cpu_count() there shows the whole machine), else the
+    affinity mask."""
+    env = os.environ.get("SATMI_CPU_CORES") or os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(env) if env else len(os.sched_getaffinity(0)))
+
+
 def cpu_baseline(batch_host, seconds, node_limit):
     """The CPU oracle (oracle/, a C restatement of REF.py's DPLL, SOUND mode) on
-    rank 0's host: one core, instances of the same batch until `seconds` pass."""
+    rank 0's host, on the same bench batch: one core (instances from the start
+    of the batch until `seconds` / 3 pass), then every core (oracle/cpu_pool.py
+    as a child process that never touches the GPU, one worker per core, for
+    `seconds`).  `value` is the all-cores rate; the one-core rate is beside it."""
+    import subprocess
+    import tempfile
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.lib()
@@ -102,16 +116,32 @@ def cpu_baseline(batch_host, seconds, node_limit):
         r = oracle.dpll(batch_host.instance(done), "sound", max_solutions=1, sol_cap=1, node_limit=node_limit)
         props += r["counters"]["unit_props"]
         done += 1
-        if time.perf_counter() - t0 > seconds:
+        if time.perf_counter() - t0 > seconds / 3:
             break
     dt = time.perf_counter() - t0
     capped = node_limit > 0
-    return {"value": props / dt if capped else done / dt, "unit": "unit-props/s" if capped else "instances/s",
-            "cores": 1, "kind": "port",
-            "sample": f"first {done} instances of the rank-0 bench batch (same n/alpha"
-                      f"{', node limit %d' % node_limit if capped else ''}), "
-                      f"oracle/sat_oracle.c SOUND mode, single thread, {dt:.1f} s",
-            "instances_per_s": done / dt, "unit_props_per_s": props / dt}
+    one = {"instances_per_s": done / dt, "unit_props_per_s": props / dt, "instances": done, "seconds": dt}
+    cores = host_cores()
+    # bounded sample for the pool: enough instances for every core for `seconds`
+    nsamp = min(batch_host.num_instances, max(4 * cores, int(4 * cores * seconds * max(done, 1) / dt)))
+    icb = batch_host.inst_clause_begin[:nsamp + 1].astype(np.int32)
+    clb = batch_host.clause_lit_begin[:int(icb[-1]) + 1].astype(np.int32)
+    lits = batch_host.lits[:int(clb[-1])].astype(np.int32)
+    with tempfile.TemporaryDirectory(prefix="satmi_cpu_") as tmp:
+        for name, arr in (("icb", icb), ("clb", clb), ("lits", lits)):
+            np.save(os.path.join(tmp, name + ".npy"), arr)
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("HIP_", "ROCR_", "HSA_"))}
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_pool.py"), tmp, str(seconds),
+                              str(node_limit), str(cores)], check=True, capture_output=True, text=True, env=env)
+    pool = json.loads(out.stdout.strip().splitlines()[-1])
+    rate = pool["unit_props_per_s"] if capped else pool["instances_per_s"]
+    return {"value": rate, "unit": "unit-props/s" if capped else "instances/s",
+            "cores": cores, "kind": "port",
+            "sample": f"{pool['instances']} instances from the start of the rank-0 bench batch (same n/alpha"
+                      f"{', node limit %d' % node_limit if capped else ''}), oracle/sat_oracle.c SOUND mode, "
+                      f"{cores} worker processes (one per host core) for {pool['seconds']:.1f} s",
+            "instances_per_s": pool["instances_per_s"], "unit_props_per_s": pool["unit_props_per_s"],
+            "single_core": one}
 
 
 def load_pmc(workload_key):
@@ -298,20 +328,26 @@ def main():
     # node-capped workloads (configs[4]) measure search throughput: unit-props/s
     value = props / elapsed if capped else all_inst / elapsed
 
-    # correctness spot check outside the timed region: every reported model satisfies its formula
-    icb, clb, lits, nv = batches[(args.steps - 1) % 2]
-    sat_rows = counters[:, 5] > 0
-    val = torch.zeros((B, n + 1), dtype=torch.int8, device=dev)
-    live = torch.arange(n, device=dev)[None, :] < sol_len[:, None]
-    idx = torch.where(live, sol_lits.abs(), 0).to(torch.int64)
-    val.scatter_(1, idx, torch.where(sol_lits > 0, 1, -1).to(torch.int8))
-    val[:, 0] = 0
-    lv = lits.view(B, m, k).to(torch.int64)
-    litval = torch.gather(val, 1, lv.abs().view(B, -1)).view(B, m, k) * torch.sign(lv).to(torch.int8)
-    clause_ok = (litval > 0).any(dim=2).all(dim=1)
-    models_ok = bool(((~sat_rows) | clause_ok).all().item())
+    # correctness check outside the timed region, on BOTH resident batches (the
+    # last step of each stream): every reported model satisfies its formula
+    def models_ok_for(j):
+        icb_, clb_, lits_, nv_ = batches[j % 2]
+        status_, counters_, sol_len_, sol_lits_ = outs[j % 2]
+        sat_rows = counters_[:, 5] > 0
+        val = torch.zeros((B, n + 1), dtype=torch.int8, device=dev)
+        live = torch.arange(n, device=dev)[None, :] < sol_len_[:, None]
+        idx = torch.where(live, sol_lits_.abs(), 0).to(torch.int64)
+        val.scatter_(1, idx, torch.where(sol_lits_ > 0, 1, -1).to(torch.int8))
+        val[:, 0] = 0
+        lv = lits_.view(B, m, k).to(torch.int64)
+        litval = torch.gather(val, 1, lv.abs().view(B, -1)).view(B, m, k) * torch.sign(lv).to(torch.int8)
+        clause_ok = (litval > 0).any(dim=2).all(dim=1)
+        return bool(((~sat_rows) | clause_ok).all().item())
+
+    models_ok = all(models_ok_for(j) for j in range(max(0, args.steps - 2), args.steps))
     if not models_ok or bad:
         raise SystemExit(f"bench: invalid result (models_ok={models_ok}, limited={bad})")
+    icb, clb, lits, nv = batches[(args.steps - 1) % 2]
 
     # roofline of the dominant kernel: algorithmic bytes per launch / average launch time
     read_bytes = B * (4 * m * k + 4 * m + 4 + 4) + 4
@@ -323,7 +359,7 @@ def main():
     kern, lds, per_cu = _capi.plan(n, m, m * k, k)
     resident = min(B, torch.cuda.get_device_properties(dev).multi_processor_count * per_cu)
     # busy wave-time over resident wave-time of the timed region (both streams)
-    util = ticks / world * 1e-8 / (resident * elapsed)
+    util = ticks / world / hz / (resident * elapsed)
     pmc = load_pmc(workload)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,

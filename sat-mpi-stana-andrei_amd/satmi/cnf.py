@@ -163,6 +163,8 @@ def uniform_ksat_device(num_instances, n, m, k, seed, device):
         if nd == 0:
             break
         vars_[dup] = torch.randint(1, n + 1, (nd, k), device=device, generator=g, dtype=torch.int32)
+    else:
+        raise RuntimeError("could not draw distinct variables")   # as uniform_ksat
     sign = torch.rand((B, m, k), device=device, generator=g) < 0.5
     lits = torch.where(sign, -vars_, vars_).reshape(-1).contiguous()
     icb = (torch.arange(B + 1, device=device, dtype=torch.int64) * m).to(torch.int32)

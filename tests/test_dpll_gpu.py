@@ -306,3 +306,55 @@ def test_snapshot_epoch_wraparound_parity():
         for key in CTR:
             assert got[key] == o["counters"][key], (b, key)
         assert r.solutions(b)[:1] == o["solutions"][:1]
+
+
+@pytest.mark.parametrize("policy", ["scan", "general"])
+def test_sound_kernels_match_reference_fixture(golden_dir, policy):
+    """Both DPLL kernels against tests/golden/dpll_sound_ref.json: the reference's
+    own dpll_optimized with only the branch of REF.py:210-213 applied as a unit
+    clause (make_golden_sound.py), at BASELINE configs[1] (n=50) and configs[2]
+    (n=100) shapes plus edge and generator formulas.  First-model search (the
+    bench's max_solutions=1): every counter and the model; full enumeration:
+    every counter and the solution count."""
+    cases = _golden(golden_dir, "dpll_sound_ref.json")
+    kern = _capi.KERNEL_SCAN if policy == "scan" else _capi.KERNEL_GENERAL
+    if policy == "scan":   # the scan kernel's shapes: clauses of 1..5 literals
+        cases = [c for c in cases if c["formula"] and all(1 <= len(cl) <= 5 for cl in c["formula"])]
+    assert sum(c["tag"] == "configs2_n100" for c in cases) >= 48
+    fs = [c["formula"] for c in cases]
+    r = _run_policy(fs, kern, max_solutions=1, sol_cap=1, time_limit=60.0)
+    for b, c in enumerate(cases):
+        got = r.counter_dict(b)
+        for k in ("nodes", "decisions", "unit_props", "pure_assigns", "conflicts"):
+            assert got[k] == c["first"]["counters"][k], (policy, c["tag"], k)
+        want = [] if c["first"]["model"] is None else [c["first"]["model"]]
+        assert r.solutions(b) == want, (policy, c["tag"])
+    full = [c for c in cases if "full" in c]
+    r = _run_policy([c["formula"] for c in full], kern, max_solutions=0, sol_cap=1, time_limit=60.0)
+    for b, c in enumerate(full):
+        assert int(r.status[b]) == _capi.DPLL_EXHAUSTED
+        got = r.counter_dict(b)
+        for k in ("nodes", "decisions", "unit_props", "pure_assigns", "conflicts"):
+            assert got[k] == c["full"]["counters"][k], (policy, c["tag"], k)
+        assert got["solutions"] == c["full"]["solutions"]
+        first = r.solutions(b)[0] if got["solutions"] else None
+        assert first == c["full"]["first_solution"], (policy, c["tag"])
+
+
+@pytest.mark.parametrize("n,m,cap", [(200, 700, 800), (300, 1100, 500)])
+def test_scan_kernel_chunk_group_tails(n, m, cap):
+    """Clause counts whose 64-clause chunks split into a 7-chunk group followed
+    by a 4-chunk group (m=700: 11 chunks; m=1100: 7+7+4 = 18 chunks) -- the
+    for_chunks path of dpll_scan.hip no other shape reaches.  Scan kernel vs
+    general kernel vs oracle, node-capped, every counter and any model."""
+    batch = cnf.uniform_ksat(6, n, m, 3, seed=n + m)
+    rs = _run_policy(batch, _capi.KERNEL_SCAN, max_solutions=1, node_limit=cap, sol_cap=1)
+    rg = _run_policy(batch, _capi.KERNEL_GENERAL, max_solutions=1, node_limit=cap, sol_cap=1)
+    assert (rs.status == rg.status).all()
+    assert (rs.counters[:, :7] == rg.counters[:, :7]).all()
+    for b in range(6):
+        o = oracle.dpll(batch.instance(b), "sound", max_solutions=1, node_limit=cap, sol_cap=1)
+        assert int(rs.status[b]) == o["status"]
+        for key in CTR:
+            assert rs.counter_dict(b)[key] == o["counters"][key], (b, key)
+        assert rs.solutions(b)[:1] == o["solutions"][:1]

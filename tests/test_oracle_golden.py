@@ -62,3 +62,34 @@ def test_sound_mode_verdicts_match_reference_dp(golden_dir):
             model = {abs(l): l > 0 for l in r["solutions"][0]}
             for cl in f:
                 assert any(model.get(abs(l)) == (l > 0) for l in cl), (f, cl)
+
+
+SOUND_CTR = ("nodes", "decisions", "unit_props", "pure_assigns", "conflicts")
+
+
+def test_sound_mode_matches_reference_rewritten_branch(golden_dir):
+    """The benchmarked SOUND semantics, pinned to the reference's own code:
+    tests/golden/dpll_sound_ref.json comes from REF.py's dpll_optimized with
+    only the branch statements of REF.py:210-213 rewritten (the branch literal
+    recursed on as the unit clause `formula + [[lit]]`; make_golden_sound.py).
+    Every counter and the first model at the first-model stop (the bench's
+    max_solutions=1), and the full enumeration where the reference finished."""
+    cases = _load(golden_dir, "dpll_sound_ref.json")
+    tags = {c["tag"] for c in cases}
+    assert {"edge", "generator", "configs1_n50", "configs2_n100"} <= tags
+    assert sum(c["tag"] == "configs2_n100" for c in cases) >= 48
+    for c in cases:
+        f = c["formula"]
+        r = oracle.dpll(f, "sound", max_solutions=1, sol_cap=1)
+        for k in SOUND_CTR:
+            assert r["counters"][k] == c["first"]["counters"][k], (c["tag"], k, f)
+        if c["first"]["model"] is None:
+            assert r["counters"]["solutions"] == 0 and r["status"] == 0
+        else:
+            assert r["solutions"][0] == c["first"]["model"], (c["tag"], f)
+        if "full" in c:
+            r = oracle.dpll(f, "sound", max_solutions=0, sol_cap=1)
+            for k in SOUND_CTR:
+                assert r["counters"][k] == c["full"]["counters"][k], (c["tag"], k, f)
+            assert r["counters"]["solutions"] == c["full"]["solutions"]
+            assert (r["solutions"][0] if r["solutions"] else None) == c["full"]["first_solution"]
