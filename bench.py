@@ -48,7 +48,8 @@ from satmi.shard import shard_range  # noqa: E402
 
 METRIC = "instances solved/sec, random 3-SAT n=100 α=4.26; unit-props/sec; HBM GB/s"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-KERNELS = {_capi.KERNEL_SCAN: "dpll_scan_kernel", _capi.KERNEL_GENERAL: "dpll_batch_kernel"}
+KERNELS = {_capi.KERNEL_SCAN: "dpll_scan_kernel", _capi.KERNEL_INC: "dpll_scan_kernel (incremental rounds)",
+           _capi.KERNEL_GENERAL: "dpll_batch_kernel"}
 
 
 # workload presets: (total instances per step, n, alpha, k, node_limit, BASELINE config)
@@ -77,6 +78,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-steps", action="store_true", help="no warmup/cpu leg (for rocprofv3 runs)")
+    p.add_argument("--kernel", choices=("auto", "inc", "scan", "general"), default="auto",
+                   help="DPLL kernel policy (satmi_dpll_set_kernel); auto = incremental clause kernel")
     a = p.parse_args()
     if a.workload in SATURATION:
         return a
@@ -238,6 +241,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     L = _capi.load()
+    _capi.set_kernel({"auto": _capi.KERNEL_AUTO, "inc": _capi.KERNEL_INC, "scan": _capi.KERNEL_SCAN,
+                      "general": _capi.KERNEL_GENERAL}[args.kernel])
 
     n, k = args.n, args.k
     b0, b1 = shard_range(args.total, world, rank)   # this rank's contiguous shard of the step's batch

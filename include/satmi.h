@@ -164,12 +164,17 @@ uint64_t satmi_dpll_lds_bytes(int max_vars, int max_clauses, int max_lits);
 uint64_t satmi_dpll_scan_lds_bytes(int max_vars, int max_clauses, int max_lits, int max_clause_len);
 
 /* Which DPLL kernel satmi_dpll_batch_* use (process-wide; default AUTO):
- *   AUTO     the clause-scan kernel where eligible, else the general kernel
- *   GENERAL  always the general (occurrence-list) kernel
- *   SCAN     the clause-scan kernel; an ineligible call fails with SATMI_ERR_ARG */
+ *   AUTO     the incremental clause kernel where eligible, else the general kernel
+ *   GENERAL  always the general (occurrence-list, clause-counter) kernel
+ *   SCAN     the clause-scan kernel, every propagation round a full clause scan;
+ *            an ineligible call fails with SATMI_ERR_ARG
+ *   INC      the clause kernel with incremental rounds (only the clauses that lost
+ *            a literal are read); an ineligible call fails with SATMI_ERR_ARG
+ * All four give identical statuses, counters and models. */
 #define SATMI_KERNEL_AUTO 0
 #define SATMI_KERNEL_GENERAL 1
 #define SATMI_KERNEL_SCAN 2
+#define SATMI_KERNEL_INC 3
 int satmi_dpll_set_kernel(int policy);
 
 /* The launch satmi_dpll_batch_device would make for this batch shape under the

@@ -880,6 +880,8 @@ static bool make_layout(int max_vars, int max_clauses, int max_lits, DpllLayout 
 // ordered, so reusing that stream's counter is safe.
 struct DeviceWork {
     std::unordered_map<hipStream_t, uint32_t *> counters;
+    // incremental scan kernel: occurrence-list scratch per stream (grown, never shrunk)
+    std::unordered_map<hipStream_t, std::pair<uint16_t *, size_t>> occ;
     double ticks_per_s = 1e8;
     bool init = false;
 };
@@ -937,8 +939,32 @@ extern "C" int satmi_wallclock_hz(double *hz) {
     return SATMI_OK;
 }
 
+// Occurrence-list scratch of the incremental kernel on `stream`: launches on one
+// stream are ordered, so a buffer is only replaced after the stream drained.
+static uint16_t *occ_scratch(hipStream_t stream, size_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_work_mu);
+    if ((int)g_work.size() <= dev) g_work.resize(dev + 1);
+    auto &slot = g_work[dev].occ[stream];
+    if (slot.second >= bytes) return slot.first;
+    if (slot.first) {
+        if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+        (void)hipFree(slot.first);
+        slot = {nullptr, 0};
+    }
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        set_error("occurrence-list scratch: hipMalloc failed");
+        return nullptr;
+    }
+    slot = {(uint16_t *)p, bytes};
+    return slot.first;
+}
+
 extern "C" int satmi_dpll_set_kernel(int policy) {
-    if (policy != SATMI_KERNEL_AUTO && policy != SATMI_KERNEL_GENERAL && policy != SATMI_KERNEL_SCAN) {
+    if (policy != SATMI_KERNEL_AUTO && policy != SATMI_KERNEL_GENERAL && policy != SATMI_KERNEL_SCAN &&
+        policy != SATMI_KERNEL_INC) {
         set_error("satmi_dpll_set_kernel: unknown policy");
         return SATMI_ERR_ARG;
     }
@@ -948,7 +974,7 @@ extern "C" int satmi_dpll_set_kernel(int policy) {
 
 extern "C" uint64_t satmi_dpll_scan_lds_bytes(int max_vars, int max_clauses, int max_lits, int max_clause_len) {
     uint32_t bytes = 0;
-    if (!dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, &bytes)) return 0;
+    if (!dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, false, &bytes)) return 0;
     return bytes;
 }
 
@@ -960,10 +986,11 @@ extern "C" int satmi_dpll_plan(int max_vars, int max_clauses, int max_lits, int 
     }
     const int policy = g_kernel_policy.load();
     uint32_t sb = 0;
+    const bool inc = policy != SATMI_KERNEL_SCAN;
     if (mode == SATMI_MODE_SOUND && !has_init && policy != SATMI_KERNEL_GENERAL &&
-        dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, &sb)) {
-        *kernel = SATMI_KERNEL_SCAN;
-        const int rc = dpll_scan_resident(max_vars, max_clauses, max_clause_len, waves_per_cu, &sb);
+        dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, inc, &sb)) {
+        *kernel = inc ? SATMI_KERNEL_INC : SATMI_KERNEL_SCAN;
+        const int rc = dpll_scan_resident(max_vars, max_clauses, max_clause_len, inc, waves_per_cu, &sb);
         *lds_bytes_per_wave = sb;
         return rc;
     }
@@ -1019,11 +1046,12 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
     // SOUND mode without a caller assignment: the clause-scan kernel
     // (dpll_scan.hip) when the batch shape fits it, unless policy says otherwise
     const int policy = g_kernel_policy.load();
+    const bool inc = policy != SATMI_KERNEL_SCAN;
     const bool scan_ok = mode == SATMI_MODE_SOUND && !d_init_begin && policy != SATMI_KERNEL_GENERAL &&
-                         dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, nullptr);
-    if (policy == SATMI_KERNEL_SCAN && !scan_ok) {
-        set_error("satmi_dpll_batch_device: SATMI_KERNEL_SCAN policy but the batch is not eligible (SOUND mode, "
-                  "no caller assignment, clause lengths 1..5, <= 2047 variables)");
+                         dpll_scan_eligible(max_vars, max_clauses, max_lits, max_clause_len, inc, nullptr);
+    if ((policy == SATMI_KERNEL_SCAN || policy == SATMI_KERNEL_INC) && !scan_ok) {
+        set_error("satmi_dpll_batch_device: SATMI_KERNEL_SCAN/INC policy but the batch is not eligible (SOUND "
+                  "mode, no caller assignment, clause lengths 1..5, <= 2047 variables)");
         return SATMI_ERR_ARG;
     }
     if (scan_ok) {
@@ -1059,6 +1087,8 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         Lc.work_counter = wc;
         Lc.num_cus = cus;
         Lc.stream = (hipStream_t)stream;
+        Lc.inc = inc;
+        Lc.occ_alloc = [stream](size_t bytes) { return occ_scratch((hipStream_t)stream, bytes); };
         SATMI_HIP(hipMemsetAsync(wc, 0, 24, Lc.stream));   // counter + launch span (common.h)
         return dpll_scan_launch(Lc);
     }

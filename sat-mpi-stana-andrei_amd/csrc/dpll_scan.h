@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
+
 namespace satmi {
 
 struct ScanLaunch {
@@ -19,15 +21,20 @@ struct ScanLaunch {
     uint32_t *work_counter;
     int num_cus;
     hipStream_t stream;
+    bool inc = false;   // incremental propagation (occurrence lists) instead of full clause scans
+    // incremental kernel: returns >= bytes of device scratch for the occurrence lists,
+    // valid for this launch on `stream` (nullptr on failure)
+    std::function<uint16_t *(size_t)> occ_alloc;
 };
 
 // Can the scan kernel take a batch of this shape (SOUND mode, no caller
 // assignment)?  Fills *lds_bytes with the per-wave LDS it would use.
-bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_clause_len, uint32_t *lds_bytes);
+bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_clause_len, bool inc,
+                        uint32_t *lds_bytes);
 
 // Waves of the scan kernel resident per CU for this shape (LDS and registers),
 // and the LDS bytes per wave of that launch (dynamic image + static literal states).
-int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu,
+int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, bool inc, int *waves_per_cu,
                        uint32_t *lds_per_wave = nullptr);
 
 // Launch on L.stream (asynchronous).  The caller has checked eligibility and

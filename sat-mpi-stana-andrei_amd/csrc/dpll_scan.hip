@@ -34,6 +34,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "common.h"
 #include "dpll_scan.h"
@@ -72,7 +73,6 @@ enum { PH_STAGE = 0, PH_ASSIGN = 1, PH_UNITS = 2, PH_CONFLICT = 3, PH_COUNTS = 4
        PH_OTHER = 7 };
 
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
-constexpr uint32_t PHASE_BIT = 0x8000u;
 
 // Literal state byte lv[code] (code = v << 1 | negative): free 1, true 8,
 // false 0.  The sum of a clause's bytes: bits 0-2 = free occurrences (REF.py's
@@ -115,8 +115,8 @@ __device__ __forceinline__ uint32_t field(typename Pack<K>::W w, int j) {
 }
 
 struct ScanLayout {
-    uint32_t cls, lv, ts, cnt, first, trail, fvar, ftrail, scratch, bytes;
-    int32_t mcap, ncap;
+    uint32_t cls, lv, ts, cnt, first, trail, fvar, ftrail, scratch, occ_off, acc, pfx, bytes;
+    int32_t mcap, ncap, nw;   // nw: 32-clause words of the unit bitmap (incremental kernel)
 };
 
 struct ScanArgs {
@@ -128,21 +128,32 @@ struct ScanArgs {
     int64_t *counters;
     int32_t *sol_len, *sol_lits, *root_len, *root_lits;
     uint32_t *work_counter;
+    uint16_t *occ;      // incremental kernel: per-wave occurrence-list scratch (HBM/L2), occ_cap entries each
+    int32_t occ_cap;
     ScanLayout lay;
 };
 
-template <int K>
+// C: the type of a literal code / variable / trail position in the trail,
+// decision frames and snapshot -- uint8_t for the 256-B size class (n <= 127),
+// which halves those arrays, else uint16_t.
+template <int K, typename C>
 struct SLds {
+    static constexpr uint32_t PHASE_BIT = 1u << (8 * sizeof(C) - 1);   // fvar: the False branch runs
     typename Pack<K>::W *cls;   // [mcap rounded up to 64]  packed literal codes per clause
     uint8_t *lv;                // [2(ncap+1)]  literal state bytes
     uint32_t *ts;               // [ncap+1]  snapshot index of the assignment in the running batch
     uint32_t *cnt;              // [ncap+1]  free occurrences in active clauses, pos | neg << 16
     uint32_t *first;            // [ncap+1]  first free occurrence, position c << 3 | slot
-    uint16_t *trail;            // [ncap+1]  assignment order (literal codes) == dict insertion order
-    uint16_t *fvar;             // [ncap+1]  decision frames: var | PHASE_BIT once False runs
-    uint16_t *ftrail;           // [ncap+1]  trail length before the decision
-    uint16_t *snap;             // scratch:  unit-clause snapshot (propagation)
+    C *trail;                   // [ncap+1]  assignment order (literal codes) == dict insertion order
+    C *fvar;                    // [ncap+1]  decision frames: var | PHASE_BIT once False runs
+    C *ftrail;                  // [ncap+1]  trail length before the decision
+    C *snap;                    // scratch:  unit-clause snapshot (propagation)
     uint32_t *plist;            // scratch:  pure-literal positions (analysis), aliases snap
+    // incremental kernel only
+    uint16_t *occ_off;          // [2(ncap+1)+1]  start of each literal code's occurrence list in `occ`
+    uint32_t *acc;              // [nw]  unit clauses found this round, one bit per clause
+    uint2 *pfx;                 // [nw]  (bits, units before the word) of the finished bitmap
+    const uint16_t *occ;        // global: clause indices holding each literal code (distinct per clause)
 };
 
 // literal `code` becomes true: one 2-byte store sets both literals of its variable
@@ -158,8 +169,8 @@ __device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return
 // its slot j), one 64-clause chunk per lane step; the loads of U chunks are
 // issued before any is used.  mpad is a multiple of 64 (dummy clauses are
 // always satisfied).
-template <int K, int U, typename F>
-__device__ __forceinline__ void chunk_group(const SLds<K> &S, int c0, F &&f) {
+template <int K, int U, typename C, typename F>
+__device__ __forceinline__ void chunk_group(const SLds<K, C> &S, int c0, F &&f) {
     using W = typename Pack<K>::W;
     const int ln = lane_id();
     W w[U];
@@ -176,8 +187,8 @@ __device__ __forceinline__ void chunk_group(const SLds<K> &S, int c0, F &&f) {
 
 // Groups of U chunks, then (U > 4) groups of 4, then single chunks: n=100's 7
 // chunks are one group of 7, n=50's 4 chunks one group of 4.
-template <int K, int U, typename F>
-__device__ __forceinline__ void for_chunks(const SLds<K> &S, int mpad, F &&f) {
+template <int K, int U, typename C, typename F>
+__device__ __forceinline__ void for_chunks(const SLds<K, C> &S, int mpad, F &&f) {
     using W = typename Pack<K>::W;
     const int ln = lane_id();
     int c0 = 0;
@@ -226,8 +237,8 @@ __device__ __forceinline__ uint32_t stamp_index(uint32_t st) { return 0xFFFFu - 
 // index (within the batch of epoch `bep` just assigned) whose assignment
 // emptied a clause first -- an emptied clause was emptied by the
 // latest-stamped of its literals (REF.py:161-162), found in the same pass.
-template <int K>
-__device__ int scan_units(const SLds<K> &S, int mpad, uint32_t ep, uint32_t bep, int *empty_at) {
+template <int K, typename C>
+__device__ int scan_units(const SLds<K, C> &S, int mpad, uint32_t ep, uint32_t bep, int *empty_at) {
     using W = typename Pack<K>::W;
     const uint64_t lt = lanemask_lt();
     int nu = 0;
@@ -252,7 +263,7 @@ __device__ int scan_units(const SLds<K> &S, int mpad, uint32_t ep, uint32_t bep,
         if (unit) {
             const uint32_t k = (uint32_t)nu + (uint32_t)__popcll(mk & lt);
             const uint32_t code = unit_code<K>(S.cls[c], x);   // re-read: keeps U words out of VGPRs
-            S.snap[k] = (uint16_t)code;
+            S.snap[k] = (C)code;
             atomicMax(&S.ts[code >> 1], stamp(ep, k));
         }
         nu += __popcll(mk);
@@ -262,10 +273,134 @@ __device__ int scan_units(const SLds<K> &S, int mpad, uint32_t ep, uint32_t bep,
     return nu;
 }
 
+// Incremental form of scan_units for every round after the first: the next
+// snapshot can only hold clauses that lost a literal in the batch just
+// assigned, trail[rs, tl) -- every unit of the previous snapshot is now
+// satisfied (or the round ended in a conflict), and no other clause changed.
+// So only the clauses on the occurrence lists of the batch's negated literals
+// are read (64 per wave step, gathered from the HBM/L2-resident lists).  Unit
+// clauses set their bit in a clause bitmap; the bitmap's prefix popcounts give
+// each unit its snapshot index, i.e. REF.py:143's clause order, with a clause
+// reached twice counted once.  Emptied clauses are found among the same
+// touched clauses (an emptied clause lost its last literal in this batch).
+// Same results as scan_units, bit for bit.
+template <int K, typename C>
+__device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t ep, uint32_t bep, int *empty_at) {
+    using W = typename Pack<K>::W;
+    const int ln = lane_id();
+    int e = INT_MAX;
+    int passes = 0;
+    bool unit = false;          // this lane found a unit clause (valid when one pass covered all touched clauses)
+    uint32_t uc = 0, ucode = 0;
+    for (int i0 = rs; i0 < tl; i0 += 64) {
+        // lane b: the b-th batch literal's negation and its occurrence list
+        const int i = i0 + ln;
+        int ob = 0, len = 0;
+        if (i < tl) {
+            const uint32_t x = (uint32_t)S.trail[i] ^ 1u;
+            ob = S.occ_off[x];
+            len = (int)S.occ_off[x + 1] - ob;
+        }
+        const int incl = wave_incl_scan(len);
+        const int excl = incl - len;
+        const int delta = ob - excl;   // touched index t of list b reads occ[delta_b + t]
+        const int total = lane63(incl);
+        const int nb = min(64, tl - i0);
+        for (int t0 = 0; t0 < total; t0 += 64) {
+            const int t = t0 + ln;
+            int d = 0;
+            for (int b = 0; b < nb; ++b) {   // segments are in order: the last that starts at or before t owns it
+                const int eb = __builtin_amdgcn_readlane(excl, b);
+                const int db = __builtin_amdgcn_readlane(delta, b);
+                d = t >= eb ? db : d;
+            }
+            ++passes;
+            if (t < total) {
+                const uint32_t c = S.occ[d + t];
+                const W w = S.cls[c];
+                uint32_t x[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) x[j] = S.lv[field<K>(w, j)];
+                const uint32_t s = clause_sum<K>(x);
+                if (!sum_true(s)) {
+                    const uint32_t nf = sum_nfree(s);
+                    if (nf == 0u) {   // emptied in this batch: by its latest-stamped literal
+                        int tt = -1;
+#pragma unroll
+                        for (int j = 0; j < K; ++j) {
+                            const uint32_t code = field<K>(w, j);
+                            const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : 0u;
+                            if ((st >> 16) == bep) tt = max(tt, (int)stamp_index(st));
+                        }
+                        e = min(e, tt);
+                    } else if (nf == 1u) {
+                        atomicOr(&S.acc[c >> 5], 1u << (c & 31u));
+                        unit = true;
+                        uc = c;
+                        ucode = unit_code<K>(w, x);
+                    }
+                }
+            }
+        }
+    }
+    wave_sync();
+    const int emp = __ballot(e != INT_MAX) ? wave_min_i32(e) : INT_MAX;
+    *empty_at = emp;
+    if (emp != INT_MAX) {   // conflict: the snapshot is not needed, only a clean bitmap
+        for (int w = ln; w < nw; w += 64) S.acc[w] = 0u;
+        wave_sync();
+        return 0;
+    }
+    // prefix popcounts of the bitmap (and clear it for the next round)
+    int nu = 0;
+    for (int w0 = 0; w0 < nw; w0 += 64) {
+        const int w = w0 + ln;
+        uint32_t bits = 0u;
+        if (w < nw) {
+            bits = S.acc[w];
+            S.acc[w] = 0u;
+        }
+        const int pc = __popc(bits);
+        const int in = wave_incl_scan(pc);
+        if (w < nw) S.pfx[w] = make_uint2(bits, (uint32_t)(nu + in - pc));
+        nu += lane63(in);
+    }
+    wave_sync();
+    if (passes <= 1) {
+        // one pass held every touched clause: each unit lane places its clause
+        if (unit) {
+            const uint2 p = S.pfx[uc >> 5];
+            const uint32_t k = p.y + (uint32_t)__popc(p.x & ((1u << (uc & 31u)) - 1u));
+            S.snap[k] = (C)ucode;
+            atomicMax(&S.ts[ucode >> 1], stamp(ep, k));
+        }
+    } else {
+        // long batch: walk the bitmap word by word, re-deriving each unit literal
+        for (int w = ln; w < nw; w += 64) {
+            const uint2 p = S.pfx[w];
+            uint32_t bits = p.x, k = p.y;
+            while (bits) {
+                const uint32_t c = ((uint32_t)w << 5) | (uint32_t)__builtin_ctz(bits);
+                bits &= bits - 1u;
+                const W wd = S.cls[c];
+                uint32_t x[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) x[j] = S.lv[field<K>(wd, j)];
+                const uint32_t code = unit_code<K>(wd, x);
+                S.snap[k] = (C)code;
+                atomicMax(&S.ts[code >> 1], stamp(ep, k));
+                ++k;
+            }
+        }
+    }
+    wave_sync();
+    return nu;
+}
+
 // The epoch of a decision snapshot.  No stamp is live between propagate calls,
 // so this is where the 16-bit epoch wraps: all stamps are reset to epoch 0.
-template <int K>
-__device__ uint32_t next_decision_epoch(const SLds<K> &S, int n, uint32_t ep) {
+template <int K, typename C>
+__device__ uint32_t next_decision_epoch(const SLds<K, C> &S, int n, uint32_t ep) {
     if (ep < EPOCH_LIMIT) return ep + 1;
     for (int v = lane_id(); v <= n; v += 64) S.ts[v] = 0u;
     wave_sync();
@@ -277,9 +412,9 @@ __device__ uint32_t next_decision_epoch(const SLds<K> &S, int n, uint32_t ep) {
 // true on conflict; `tl` ends where the reference stops (the assignments it
 // made, including the one that emptied a clause).  `dec`: the first batch is
 // the decision literal, which REF.py's counters do not count as a propagation.
-template <int K>
-__device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec, uint32_t &ep, int64_t &props,
-                          int64_t &rounds, PhaseClock &ph) {
+template <int K, bool INC, typename C>
+__device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool dec, uint32_t &ep, uint32_t &props,
+                          uint32_t &rounds, PhaseClock &ph) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     while (nu > 0) {
@@ -294,7 +429,7 @@ __device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec,
             const bool first = valid && S.ts[v] == stamp(bep, (uint32_t)k);
             const uint64_t mk = __ballot(first);
             if (first) {
-                S.trail[tl + __popcll(mk & lt)] = (uint16_t)code;
+                S.trail[tl + __popcll(mk & lt)] = (C)code;
                 lv_assign(S.lv, code);
             }
             tl += __popcll(mk);
@@ -303,7 +438,8 @@ __device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec,
         ph.mark(PH_ASSIGN);
         const int nassign = tl - rs;
         int e = INT_MAX;
-        const int nu_next = scan_units<K>(S, mpad, ++ep, bep, &e);
+        const int nu_next = INC ? inc_units<K>(S, (mpad + 31) >> 5, rs, tl, ++ep, bep, &e)
+                                : scan_units<K>(S, mpad, ++ep, bep, &e);
         ph.mark(PH_UNITS);
         if (e != INT_MAX) {
             // the reference stopped at snapshot index e: keep the prefix of the
@@ -336,8 +472,8 @@ __device__ bool propagate(const SLds<K> &S, int mpad, int &tl, int nu, bool dec,
 // Within an active clause the atomics run for every slot -- a falsified slot
 // adds 0 / mins NONE32, padding hits variable 0 (never read) -- so there is
 // no branch per slot.
-template <int K>
-__device__ int scan_counts(const SLds<K> &S, int mpad) {
+template <int K, typename C>
+__device__ int scan_counts(const SLds<K, C> &S, int mpad) {
     using W = typename Pack<K>::W;
     int nact = 0;
     for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int c, W w, const uint32_t(&x)[K]) {
@@ -365,8 +501,8 @@ struct Choice {
 // pure_literals (REF.py:181-184) into plist (first positions), else the
 // branching variable: max(var_counts.items(), key=count), the first maximal
 // key in dict order (REF.py:208).  Clears cnt / first for the next scan.
-template <int K>
-__device__ Choice choose(const SLds<K> &S, int n) {
+template <int K, typename C>
+__device__ Choice choose(const SLds<K, C> &S, int n) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     int npure = 0;
@@ -410,8 +546,8 @@ __device__ Choice choose(const SLds<K> &S, int n) {
 
 // Append the pure literals in first-occurrence order (REF.py:187-189); the
 // literal at a pure variable's first position carries its (only) sign.
-template <int K>
-__device__ int assign_pures(const SLds<K> &S, int npure, int tl) {
+template <int K, typename C>
+__device__ int assign_pures(const SLds<K, C> &S, int npure, int tl) {
     const int ln = lane_id();
     for (int i0 = 0; i0 < npure; i0 += 64) {
         const int i = i0 + ln;
@@ -420,7 +556,7 @@ __device__ int assign_pures(const SLds<K> &S, int npure, int tl) {
         for (int j = 0; j < npure; ++j) rank += S.plist[j] < my ? 1 : 0;
         if (i < npure) {
             const uint32_t code = field<K>(S.cls[my >> 3], (int)(my & 7u));
-            S.trail[tl + rank] = (uint16_t)code;
+            S.trail[tl + rank] = (C)code;
             lv_assign(S.lv, code);
         }
     }
@@ -428,8 +564,8 @@ __device__ int assign_pures(const SLds<K> &S, int npure, int tl) {
     return tl + npure;
 }
 
-template <int K>
-__device__ void store_assignment(const SLds<K> &S, int tl, int32_t *out) {
+template <int K, typename C>
+__device__ void store_assignment(const SLds<K, C> &S, int tl, int32_t *out) {
     for (int i = lane_id(); i < tl; i += 64) {
         const uint32_t code = S.trail[i];
         const int v = (int)(code >> 1);
@@ -439,8 +575,95 @@ __device__ void store_assignment(const SLds<K> &S, int tl, int32_t *out) {
 
 enum { ST_PROPAGATE = 0, ST_ANALYZE = 1, ST_BACKTRACK = 2, ST_DONE = 3 };
 
-template <int K>
-__device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
+// Incremental kernel: occurrence lists of the staged clauses, S.occ[S.occ_off[x] ..
+// S.occ_off[x+1]) = the clauses holding literal code x (each clause once, in no
+// particular order -- the unit bitmap restores clause order).  cnt is borrowed
+// as the per-variable counter / fill cursor and left zeroed.
+template <int K, typename C>
+__device__ void build_occurrences(const SLds<K, C> &S, uint16_t *occ, int m, int n) {
+    using W = typename Pack<K>::W;
+    const int ln = lane_id();
+    // distinct slots of a clause: a repeated code counts once
+    auto each_slot = [&](auto &&f) {
+        for (int c = ln; c < m; c += 64) {
+            const W w = S.cls[c];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint32_t code = field<K>(w, j);
+                bool dup = code <= CODE_DUMMY;
+#pragma unroll
+                for (int i = 0; i < j; ++i) dup |= field<K>(w, i) == code;
+                if (!dup) f(c, code);
+            }
+        }
+    };
+    each_slot([&](int, uint32_t code) { atomicAdd(&S.cnt[code >> 1], (code & 1u) ? 0x10000u : 1u); });
+    wave_sync();
+    int carry = 0;
+    for (int v0 = 0; v0 <= n; v0 += 64) {
+        const int v = v0 + ln;
+        const uint32_t cv = v <= n ? S.cnt[v] : 0u;
+        const int p = (int)(cv & 0xFFFFu), q = (int)(cv >> 16);
+        const int in = wave_incl_scan(p + q);
+        if (v <= n) {
+            const int ex = carry + in - (p + q);
+            S.occ_off[2 * v] = (uint16_t)ex;
+            S.occ_off[2 * v + 1] = (uint16_t)(ex + p);
+            S.cnt[v] = 0u;
+        }
+        carry += lane63(in);
+    }
+    if (ln == 0) S.occ_off[2 * (n + 1)] = (uint16_t)carry;
+    wave_sync();
+    each_slot([&](int c, uint32_t code) {
+        const uint32_t old = atomicAdd(&S.cnt[code >> 1], (code & 1u) ? 0x10000u : 1u);
+        occ[S.occ_off[code] + ((old >> ((code & 1u) << 4)) & 0xFFFFu)] = (uint16_t)c;
+    });
+    wave_sync();
+    for (int v = ln; v <= n; v += 64) S.cnt[v] = 0u;
+    // the lists are read back by this wave only: complete the stores first
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_sync();
+}
+
+// Per-instance counters between flushes (see solve_instance).
+struct Ctr32 {
+    uint32_t nodes = 0, decisions = 0, props = 0, pures = 0, conflicts = 0, rounds = 0;
+};
+constexpr uint32_t FLUSH_NODES = 1u << 20;   // props per flush <= 2^20 x n < 2^32
+constexpr uint32_t TIME_CHECK_NODES = 1024;
+
+// Add the 32-bit counters into the instance's int64 row (the first flush
+// stores), zero them, and return the instance's node total so far.
+__device__ uint64_t flush_counters(int64_t *ctr, Ctr32 &c, bool &flushed) {
+    uint64_t total = 0;
+    if (lane_id() == 0) {
+        const uint32_t v[6] = {c.nodes, c.decisions, c.props, c.pures, c.conflicts, c.rounds};
+        const int k[6] = {SATMI_CTR_NODES, SATMI_CTR_DECISIONS, SATMI_CTR_UNIT_PROPS, SATMI_CTR_PURE,
+                          SATMI_CTR_CONFLICTS, SATMI_CTR_ROUNDS};
+        if (!flushed) {
+            for (int i = 0; i < 6; ++i) ctr[k[i]] = (int64_t)v[i];
+            total = c.nodes;
+        } else {
+            total = atomicAdd((unsigned long long *)&ctr[SATMI_CTR_NODES], (unsigned long long)c.nodes) + c.nodes;
+            for (int i = 1; i < 6; ++i) atomicAdd((unsigned long long *)&ctr[k[i]], (unsigned long long)v[i]);
+        }
+    }
+    flushed = true;
+    c = Ctr32{};
+    return (uint64_t)uniform_u32((uint32_t)total) | ((uint64_t)uniform_u32((uint32_t)(total >> 32)) << 32);
+}
+
+// Nodes (counted from the last flush, at which the instance had `total`) after
+// which the node loop stops for its rare checks.
+__device__ uint32_t next_event_after(const ScanArgs &A, uint64_t total) {
+    uint64_t ev = A.time_limit_ticks ? TIME_CHECK_NODES : FLUSH_NODES;
+    if (A.node_limit > 0) ev = min(ev, (uint64_t)A.node_limit + 1u - total);   // total <= node_limit here
+    return (uint32_t)ev;
+}
+
+template <int K, bool INC, typename C>
+__device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b) {
     using W = typename Pack<K>::W;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const int ln = lane_id();
@@ -452,7 +675,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
     const int L = A.clause_lit_begin[ce] - A.clause_lit_begin[cb];
     const int n = A.inst_nvars[b];
     int64_t *ctr = A.counters + (int64_t)b * SATMI_NCOUNTERS;
-    bool bad = m > A.lay.mcap || n > A.lay.ncap || n < 0 || L > 65535;
+    bool bad = m > A.lay.mcap || n > A.lay.ncap || n < 0 || L > 65535 || (INC && L > A.occ_cap);
     if (!bad) {
         // ---- stage: pack each clause's literal codes into one word
         for (int c = ln; c < mpad; c += 64) {
@@ -495,6 +718,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
         return;
     }
     wave_sync();
+    if constexpr (INC) build_occurrences<K>(S, const_cast<uint16_t *>(S.occ), m, n);
     ph.mark(PH_STAGE);
 
     // root snapshot: the input's unit clauses in order (no clause is empty yet)
@@ -502,31 +726,39 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
     uint32_t ep = 1;
     int nu = scan_units<K>(S, mpad, ep, 0u, &root_empty);
     ph.mark(PH_UNITS);
-    int64_t nodes = 1, decisions = 0, props = 0, pures = 0, conflicts = 0, sols = 0, rounds = 0;
+    // Counters since the last flush, 32-bit (few live registers in the node
+    // loop); flush_counters() adds them into the instance's int64 row.  The
+    // node loop compares one counter against next_event: the node limit, the
+    // next time check or the next flush, whichever comes first.
+    Ctr32 c;
+    c.nodes = 1;
+    int64_t sols = 0;
+    bool flushed = false;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t next_event = next_event_after(A, 0);
     int depth = 0, tl = 0;
     int status = SATMI_DPLL_EXHAUSTED;
-    bool dec_round = false, at_root = true;
-    int state = ST_PROPAGATE;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int state;
+    {
+        const bool conflict = propagate<K, INC, C>(S, mpad, tl, nu, false, ep, c.props, c.rounds, ph);
+        if (A.root_lits) store_assignment<K>(S, tl, A.root_lits + (int64_t)b * A.sol_stride);
+        if (A.root_len && ln == 0) A.root_len[b] = tl;
+        c.conflicts += conflict ? 1u : 0u;
+        state = conflict ? ST_DONE : ST_ANALYZE;   // a root conflict has nothing to backtrack to
+    }
+    bool dec_round = false;
 
     while (state != ST_DONE) {
         if (state == ST_PROPAGATE) {
-            const bool conflict = propagate<K>(S, mpad, tl, nu, dec_round, ep, props, rounds, ph);
+            const bool conflict = propagate<K, INC, C>(S, mpad, tl, nu, dec_round, ep, c.props, c.rounds, ph);
             dec_round = false;
-            if (at_root) {
-                at_root = false;
-                if (A.root_lits) store_assignment<K>(S, tl, A.root_lits + (int64_t)b * A.sol_stride);
-                if (A.root_len && ln == 0) A.root_len[b] = tl;
-            }
             if (conflict) {
-                ++conflicts;
+                ++c.conflicts;
                 state = ST_BACKTRACK;
             } else {
                 state = ST_ANALYZE;
             }
-            continue;
-        }
-        if (state == ST_ANALYZE) {
+        } else if (state == ST_ANALYZE) {
             bool leaf = false;
             Choice r{0, 0u};
             ph.mark(PH_OTHER);
@@ -542,26 +774,25 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
             if (!leaf && r.npure > 0) {                        // REF.py:186-195
                 tl = assign_pures<K>(S, r.npure, tl);
                 ph.mark(PH_PURE);
-                pures += r.npure;
-                ++nodes;                                       // recursive call; its unit_propagate is a no-op
+                c.pures += (uint32_t)r.npure;
+                ++c.nodes;                                     // recursive call; its unit_propagate is a no-op
             } else if (!leaf) {                                // REF.py:208-213, as formula + [[var]]
                 const uint32_t v = r.best_var;
                 ep = next_decision_epoch<K>(S, n, ep);
                 if (ln == 0) {
-                    S.fvar[depth] = (uint16_t)v;
-                    S.ftrail[depth] = (uint16_t)tl;
-                    S.snap[0] = (uint16_t)(v << 1);            // True first
+                    S.fvar[depth] = (C)v;
+                    S.ftrail[depth] = (C)tl;
+                    S.snap[0] = (C)(v << 1);                   // True first
                     S.ts[v] = stamp(ep, 0u);
                 }
                 ++depth;
-                ++decisions;
-                ++nodes;
+                ++c.decisions;
+                ++c.nodes;
                 nu = 1;
                 dec_round = true;
                 state = ST_PROPAGATE;
                 wave_sync();
-            }
-            if (leaf) {
+            } else {
                 if (sols < A.sol_cap) {
                     store_assignment<K>(S, tl, A.sol_lits + ((int64_t)b * A.sol_cap + sols) * A.sol_stride);
                     if (ln == 0) A.sol_len[(int64_t)b * A.sol_cap + sols] = tl;
@@ -584,15 +815,15 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
                 for (int i = ft + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
                 tl = ft;
                 wave_sync();
-                if (!(fv & PHASE_BIT)) {
+                if (!(fv & SLds<K, C>::PHASE_BIT)) {
                     ep = next_decision_epoch<K>(S, n, ep);
                     if (ln == 0) {
-                        S.fvar[top] = (uint16_t)(fv | PHASE_BIT);
-                        S.snap[0] = (uint16_t)((fv << 1) | 1u);    // False
+                        S.fvar[top] = (C)(fv | SLds<K, C>::PHASE_BIT);
+                        S.snap[0] = (C)((fv << 1) | 1u);           // False
                         S.ts[fv] = stamp(ep, 0u);
                     }
-                    ++decisions;
-                    ++nodes;
+                    ++c.decisions;
+                    ++c.nodes;
                     nu = 1;
                     dec_round = true;
                     state = ST_PROPAGATE;
@@ -602,13 +833,16 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
                 --depth;
             }
         }
-        if (state != ST_DONE) {
-            if (A.node_limit > 0 && nodes > A.node_limit) {
+        if (__builtin_expect(c.nodes >= next_event, 0) && state != ST_DONE) {
+            const uint64_t total = flush_counters(ctr, c, flushed);
+            if (A.node_limit > 0 && total > (uint64_t)A.node_limit) {
                 status = SATMI_DPLL_NODE_LIMIT;
                 state = ST_DONE;
             } else if (A.time_limit_ticks && __builtin_amdgcn_s_memrealtime() - t0 > A.time_limit_ticks) {
                 status = SATMI_DPLL_TIMEOUT;
                 state = ST_DONE;
+            } else {
+                next_event = next_event_after(A, total);
             }
         }
     }
@@ -617,15 +851,10 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
     if (A.root_lits && A.sol_stride >= 16 && ln < 8)
         ((int64_t *)(A.root_lits + (int64_t)b * A.sol_stride))[ln] = (int64_t)ph.acc[ln];
 #endif
+    flush_counters(ctr, c, flushed);
     if (ln == 0) {
         A.status[b] = status;
-        ctr[SATMI_CTR_NODES] = nodes;
-        ctr[SATMI_CTR_DECISIONS] = decisions;
-        ctr[SATMI_CTR_UNIT_PROPS] = props;
-        ctr[SATMI_CTR_PURE] = pures;
-        ctr[SATMI_CTR_CONFLICTS] = conflicts;
         ctr[SATMI_CTR_SOLUTIONS] = sols;
-        ctr[SATMI_CTR_ROUNDS] = rounds;
         ctr[SATMI_CTR_TICKS] = (int64_t)(__builtin_amdgcn_s_memrealtime() - t_start);
     }
 }
@@ -637,11 +866,13 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K> &S, int b) {
 // addresses lv[code] with the code register and an immediate offset (no
 // per-wave base add per literal).  LVS = 0: multi-wave workgroups, the waves
 // taking consecutive images of the dynamic LDS, lv included.
-template <int K, int LVS>
+template <int K, int LVS, bool INC>
 __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpll_scan_kernel(ScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char *base = LVS ? smem : smem + (size_t)(threadIdx.x >> 6) * A.lay.bytes;
-    SLds<K> S;
+    using C = std::conditional_t<LVS == 256, uint8_t, uint16_t>;
+    const int wave = (int)(threadIdx.x >> 6);
+    unsigned char *base = LVS ? smem : smem + (size_t)wave * A.lay.bytes;
+    SLds<K, C> S;
     S.cls = (typename Pack<K>::W *)(base + A.lay.cls);
     if constexpr (LVS > 0) {
         __shared__ __attribute__((aligned(16))) uint8_t lv_static[LVS];
@@ -652,18 +883,26 @@ __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpl
     S.ts = (uint32_t *)(base + A.lay.ts);
     S.cnt = (uint32_t *)(base + A.lay.cnt);
     S.first = (uint32_t *)(base + A.lay.first);
-    S.trail = (uint16_t *)(base + A.lay.trail);
-    S.fvar = (uint16_t *)(base + A.lay.fvar);
-    S.ftrail = (uint16_t *)(base + A.lay.ftrail);
-    S.snap = (uint16_t *)(base + A.lay.scratch);
+    S.trail = (C *)(base + A.lay.trail);
+    S.fvar = (C *)(base + A.lay.fvar);
+    S.ftrail = (C *)(base + A.lay.ftrail);
+    S.snap = (C *)(base + A.lay.scratch);
     S.plist = (uint32_t *)(base + A.lay.scratch);
+    if constexpr (INC) {
+        S.occ_off = (uint16_t *)(base + A.lay.occ_off);
+        S.acc = (uint32_t *)(base + A.lay.acc);
+        S.pfx = (uint2 *)(base + A.lay.pfx);
+        S.occ = A.occ + ((size_t)blockIdx.x * (blockDim.x >> 6) + (size_t)wave) * (size_t)A.occ_cap;
+        for (int w = lane_id(); w < A.lay.nw; w += 64) S.acc[w] = 0u;
+        wave_sync();
+    }
     span_begin(A.work_counter);
     for (;;) {
         uint32_t b = 0;
         if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
         b = uniform_u32(b);
         if (b >= (uint32_t)A.num_instances) break;
-        solve_instance<K>(A, S, (int)b);
+        solve_instance<K, INC, C>(A, S, (int)b);
         wave_sync();
     }
     span_end(A.work_counter);
@@ -686,34 +925,42 @@ int pick_k(int max_vars, int max_clause_len) {
     return 0;
 }
 
-bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, ScanLayout *lay) {
+// cb: bytes of a trail / frame / snapshot entry (1 for the 256-B size class, see SLds)
+bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, bool inc, uint32_t cb, ScanLayout *lay) {
     if (max_vars < 0 || max_clauses < 0 || max_clauses > 65534) return false;
     const uint32_t N = (uint32_t)max_vars + 1, M = (uint32_t)max_clauses + 1;
     const uint32_t Mpad = (uint32_t)padded_clauses(max_clauses);
+    const uint32_t NW = (Mpad + 31u) / 32u;
     uint32_t o = 0;
     lay->lv = o;      o = align16(o + (with_lv ? 2 * N : 0u));   // one-wave kernel: static LDS instead
     lay->cls = o;     o = align16(o + (K == 3 ? 4u : 8u) * Mpad);
     lay->ts = o;      o = align16(o + 4 * N);
     lay->cnt = o;     o = align16(o + 4 * N);
     lay->first = o;   o = align16(o + 4 * N);
-    lay->trail = o;   o = align16(o + 2 * N);
-    lay->fvar = o;    o = align16(o + 2 * N);
-    lay->ftrail = o;  o = align16(o + 2 * N);
-    lay->scratch = o; o = align16(o + std::max(2 * M, 4 * N));
+    lay->trail = o;   o = align16(o + cb * N);
+    lay->fvar = o;    o = align16(o + cb * N);
+    lay->ftrail = o;  o = align16(o + cb * N);
+    lay->scratch = o; o = align16(o + std::max(cb * M, 4 * N));
+    lay->occ_off = o; o = align16(o + (inc ? 2 * (2 * N + 1) : 0u));
+    lay->acc = o;     o = align16(o + (inc ? 4 * NW : 0u));
+    lay->pfx = o;     o = align16(o + (inc ? 8 * NW : 0u));
     lay->bytes = o;
     lay->mcap = max_clauses;
     lay->ncap = max_vars;
+    lay->nw = (int32_t)NW;
     return o <= 160u * 1024u;
 }
 
+template <bool INC>
 const void *scan_fn(int K, int lvs) {
     if (K == 3) {
-        if (lvs == 256) return (const void *)dpll_scan_kernel<3, 256>;
-        if (lvs == 1024) return (const void *)dpll_scan_kernel<3, 1024>;
-        return (const void *)dpll_scan_kernel<3, 0>;
+        if (lvs == 256) return (const void *)dpll_scan_kernel<3, 256, INC>;
+        if (lvs == 1024) return (const void *)dpll_scan_kernel<3, 1024, INC>;
+        return (const void *)dpll_scan_kernel<3, 0, INC>;
     }
-    return lvs ? (const void *)dpll_scan_kernel<5, 4096> : (const void *)dpll_scan_kernel<5, 0>;
+    return lvs ? (const void *)dpll_scan_kernel<5, 4096, INC> : (const void *)dpll_scan_kernel<5, 0, INC>;
 }
+const void *scan_fn(int K, int lvs, bool inc) { return inc ? scan_fn<true>(K, lvs) : scan_fn<false>(K, lvs); }
 
 struct ScanPlan {
     int waves_per_wg = 1, wg_per_cu = 1, lvs = 0;
@@ -724,13 +971,13 @@ struct ScanPlan {
 // LDS (<= 32 waves per CU) and the kernel's register budget
 // (hipOccupancyMaxActiveBlocksPerMultiprocessor); one-wave workgroups (the
 // cheaper gather addressing) whenever they reach the same residency.
-int scan_plan(int K, int max_vars, int max_clauses, ScanPlan *P) {
+int scan_plan(int K, int max_vars, int max_clauses, bool inc, ScanPlan *P) {
     int best = 0;
     for (int wpg : {1, 4, 2}) {
         const int lvs = wpg == 1 ? lv_static_class(K, max_vars) : 0;
         ScanLayout lay;
-        if (!make_layout(K, max_vars, max_clauses, lvs == 0, &lay)) continue;
-        const void *fn = scan_fn(K, lvs);
+        if (!make_layout(K, max_vars, max_clauses, lvs == 0, inc, lvs == 256 ? 1u : 2u, &lay)) continue;
+        const void *fn = scan_fn(K, lvs, inc);
         const uint32_t wg_lds = lay.bytes * (uint32_t)wpg;
         const uint32_t wg_all = wg_lds + (uint32_t)lvs;
         if (wg_all > 160u * 1024u) continue;
@@ -756,23 +1003,38 @@ int scan_plan(int K, int max_vars, int max_clauses, ScanPlan *P) {
     return SATMI_OK;
 }
 
+template <bool INC>
+void launch_kernel(int K, int lvs, dim3 g, dim3 blk, uint32_t wg_lds, hipStream_t s, const ScanArgs &A) {
+    if (K == 3 && lvs == 256)
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 256, INC>), g, blk, wg_lds, s, A);
+    else if (K == 3 && lvs == 1024)
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 1024, INC>), g, blk, wg_lds, s, A);
+    else if (K == 3)
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 0, INC>), g, blk, wg_lds, s, A);
+    else if (lvs)
+        hipLaunchKernelGGL((dpll_scan_kernel<5, 4096, INC>), g, blk, wg_lds, s, A);
+    else
+        hipLaunchKernelGGL((dpll_scan_kernel<5, 0, INC>), g, blk, wg_lds, s, A);
+}
+
 }  // namespace
 
-bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_clause_len, uint32_t *lds_bytes) {
+bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_clause_len, bool inc,
+                        uint32_t *lds_bytes) {
     const int K = pick_k(max_vars, max_clause_len);
     if (!K || max_lits > 65535) return false;
     ScanLayout lay;
-    if (!make_layout(K, max_vars, max_clauses, true, &lay)) return false;
+    if (!make_layout(K, max_vars, max_clauses, true, inc, 2u, &lay)) return false;
     if (lds_bytes) *lds_bytes = lay.bytes;
     return true;
 }
 
-int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *waves_per_cu,
+int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, bool inc, int *waves_per_cu,
                        uint32_t *lds_per_wave) {
     const int K = pick_k(max_vars, max_clause_len);
     if (!K) return SATMI_ERR_ARG;
     ScanPlan P;
-    const int rc = scan_plan(K, max_vars, max_clauses, &P);
+    const int rc = scan_plan(K, max_vars, max_clauses, inc, &P);
     if (rc) return rc;
     *waves_per_cu = P.waves_per_wg * P.wg_per_cu;
     if (lds_per_wave) *lds_per_wave = P.lay.bytes + (uint32_t)P.lvs;
@@ -782,11 +1044,11 @@ int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, int *w
 int dpll_scan_launch(const ScanLaunch &L) {
     const int K = pick_k(L.max_vars, L.max_clause_len);
     ScanPlan P;
-    if (!K || !dpll_scan_eligible(L.max_vars, L.max_clauses, L.max_lits, L.max_clause_len, nullptr)) {
+    if (!K || !dpll_scan_eligible(L.max_vars, L.max_clauses, L.max_lits, L.max_clause_len, L.inc, nullptr)) {
         set_error("dpll_scan_launch: batch shape not eligible for the scan kernel");
         return SATMI_ERR_ARG;
     }
-    const int prc = scan_plan(K, L.max_vars, L.max_clauses, &P);
+    const int prc = scan_plan(K, L.max_vars, L.max_clauses, L.inc, &P);
     if (prc) return prc;
     const ScanLayout &lay = P.lay;
     const int waves_per_wg = P.waves_per_wg;
@@ -812,18 +1074,22 @@ int dpll_scan_launch(const ScanLaunch &L) {
     A.root_len = L.root_len;
     A.root_lits = L.root_lits;
     A.work_counter = L.work_counter;
+    A.occ = nullptr;
+    A.occ_cap = 0;
     A.lay = lay;
+    if (L.inc) {
+        // occurrence lists: max_lits entries (rounded to 128 B) per resident wave
+        A.occ_cap = (std::max(L.max_lits, 1) + 63) & ~63;
+        const size_t bytes = (size_t)grid * (size_t)waves_per_wg * (size_t)A.occ_cap * sizeof(uint16_t);
+        A.occ = L.occ_alloc ? L.occ_alloc(bytes) : nullptr;
+        if (!A.occ) {
+            set_error("dpll_scan_launch: no occurrence-list scratch for the incremental kernel");
+            return SATMI_ERR_NOMEM;
+        }
+    }
     const dim3 g(grid), blk(64 * waves_per_wg);
-    if (K == 3 && P.lvs == 256)
-        hipLaunchKernelGGL((dpll_scan_kernel<3, 256>), g, blk, wg_lds, L.stream, A);
-    else if (K == 3 && P.lvs == 1024)
-        hipLaunchKernelGGL((dpll_scan_kernel<3, 1024>), g, blk, wg_lds, L.stream, A);
-    else if (K == 3)
-        hipLaunchKernelGGL((dpll_scan_kernel<3, 0>), g, blk, wg_lds, L.stream, A);
-    else if (P.lvs)
-        hipLaunchKernelGGL((dpll_scan_kernel<5, 4096>), g, blk, wg_lds, L.stream, A);
-    else
-        hipLaunchKernelGGL((dpll_scan_kernel<5, 0>), g, blk, wg_lds, L.stream, A);
+    if (L.inc) launch_kernel<true>(K, P.lvs, g, blk, wg_lds, L.stream, A);
+    else launch_kernel<false>(K, P.lvs, g, blk, wg_lds, L.stream, A);
     SATMI_HIP(hipGetLastError());
     return SATMI_OK;
 }

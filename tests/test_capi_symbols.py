@@ -55,10 +55,19 @@ def test_scan_kernel_eligibility_query():
     # the plan follows the policy: REF mode and caller assignments use the general kernel
     assert _capi.plan(100, 426, 1278, 3, _capi.MODE_REF)[0] == _capi.KERNEL_GENERAL
     assert _capi.plan(100, 426, 1278, 3, _capi.MODE_SOUND, has_init=True)[0] == _capi.KERNEL_GENERAL
-    kern, lds, _ = _capi.plan(100, 426, 1278, 3)
+    kern, lds_inc, _ = _capi.plan(100, 426, 1278, 3)
+    assert kern == _capi.KERNEL_INC    # SOUND mode default: incremental rounds
+    _capi.set_kernel(_capi.KERNEL_SCAN)
+    try:
+        kern, lds, _ = _capi.plan(100, 426, 1278, 3)
+    finally:
+        _capi.set_kernel(_capi.KERNEL_AUTO)
     # the launch's real per-wave LDS: one-wave workgroups keep the literal states
-    # in a 256-B static array instead of the image's 2(n+1) = 202 B (+ alignment)
-    assert kern == _capi.KERNEL_SCAN and s100 - 208 + 256 == lds
+    # in a 256-B static array instead of the image's 2(n+1) = 202 B (+ alignment),
+    # and (n <= 127) byte-wide trail / frames / snapshot: 3 x (208 - 112) + (864 - 432)
+    assert kern == _capi.KERNEL_SCAN and s100 - 208 + 256 - 3 * 96 - 432 == lds
+    # + occurrence-list offsets (2(2n+3) B) and the unit bitmap / its prefixes (14 x 12 B)
+    assert lds_inc == lds + 416 + 64 + 112
     _capi.set_kernel(_capi.KERNEL_GENERAL)
     try:
         assert _capi.plan(100, 426, 1278, 3)[0] == _capi.KERNEL_GENERAL

@@ -196,14 +196,15 @@ def test_scan_kernel_matches_general_and_oracle(seed, nmax, kmax, mmax):
     oracle: SOUND mode, first model and full enumeration, every counter."""
     fs = _random_mix(seed, 240, nmax, kmax, mmax)
     for maxs, cap in ((1, 1), (0, 32)):
-        rs = _run_policy(fs, _capi.KERNEL_SCAN, max_solutions=maxs, sol_cap=cap, time_limit=20.0)
         rg = _run_policy(fs, _capi.KERNEL_GENERAL, max_solutions=maxs, sol_cap=cap, time_limit=20.0)
-        assert (rs.status == rg.status).all()
-        assert (rs.counters[:, :7] == rg.counters[:, :7]).all()
-        assert (rs.root_len == rg.root_len).all()
-        for b, f in enumerate(fs):
-            assert rs.solutions(b) == rg.solutions(b), f
-            assert rs.root_assignment(b) == rg.root_assignment(b)
+        for kern in (_capi.KERNEL_SCAN, _capi.KERNEL_INC):
+            rs = _run_policy(fs, kern, max_solutions=maxs, sol_cap=cap, time_limit=20.0)
+            assert (rs.status == rg.status).all()
+            assert (rs.counters[:, :7] == rg.counters[:, :7]).all()
+            assert (rs.root_len == rg.root_len).all()
+            for b, f in enumerate(fs):
+                assert rs.solutions(b) == rg.solutions(b), (kern, f)
+                assert rs.root_assignment(b) == rg.root_assignment(b)
         for b in range(0, len(fs), 7):
             o = oracle.dpll(fs[b], "sound", max_solutions=maxs, sol_cap=cap)
             for key in CTR:
@@ -213,23 +214,25 @@ def test_scan_kernel_matches_general_and_oracle(seed, nmax, kmax, mmax):
 
 def test_scan_kernel_full_size_matches_general():
     batch = cnf.uniform_ksat(2048, 100, 426, 3, seed=77)
-    rs = _run_policy(batch, _capi.KERNEL_SCAN, max_solutions=1, sol_cap=1)
     rg = _run_policy(batch, _capi.KERNEL_GENERAL, max_solutions=1, sol_cap=1)
-    assert (rs.status == rg.status).all()
-    assert (rs.counters[:, :7] == rg.counters[:, :7]).all()
-    assert (rs.sol_lits == rg.sol_lits).all()
+    for kern in (_capi.KERNEL_SCAN, _capi.KERNEL_INC):
+        rs = _run_policy(batch, kern, max_solutions=1, sol_cap=1)
+        assert (rs.status == rg.status).all()
+        assert (rs.counters[:, :7] == rg.counters[:, :7]).all()
+        assert (rs.sol_lits == rg.sol_lits).all()
 
 
 def test_scan_policy_rejects_ineligible():
     f = [[1, 2], [-1, 2], []]
-    _capi.set_kernel(_capi.KERNEL_SCAN)
-    try:
-        with pytest.raises(_capi.SatmiError):
-            dpll_batch([f], mode="sound", max_solutions=1)      # an empty clause
-        with pytest.raises(_capi.SatmiError):
-            dpll_batch([[[1, 2]]], mode="ref", max_solutions=0)  # REF mode
-    finally:
-        _capi.set_kernel(_capi.KERNEL_AUTO)
+    for kern in (_capi.KERNEL_SCAN, _capi.KERNEL_INC):
+        _capi.set_kernel(kern)
+        try:
+            with pytest.raises(_capi.SatmiError):
+                dpll_batch([f], mode="sound", max_solutions=1)      # an empty clause
+            with pytest.raises(_capi.SatmiError):
+                dpll_batch([[[1, 2]]], mode="ref", max_solutions=0)  # REF mode
+        finally:
+            _capi.set_kernel(_capi.KERNEL_AUTO)
 
 
 def test_scan_broken_length_promise_is_too_large():
@@ -308,7 +311,7 @@ def test_snapshot_epoch_wraparound_parity():
         assert r.solutions(b)[:1] == o["solutions"][:1]
 
 
-@pytest.mark.parametrize("policy", ["scan", "general"])
+@pytest.mark.parametrize("policy", ["scan", "inc", "general"])
 def test_sound_kernels_match_reference_fixture(golden_dir, policy):
     """Both DPLL kernels against tests/golden/dpll_sound_ref.json: the reference's
     own dpll_optimized with only the branch of REF.py:210-213 applied as a unit
@@ -317,8 +320,8 @@ def test_sound_kernels_match_reference_fixture(golden_dir, policy):
     bench's max_solutions=1): every counter and the model; full enumeration:
     every counter and the solution count."""
     cases = _golden(golden_dir, "dpll_sound_ref.json")
-    kern = _capi.KERNEL_SCAN if policy == "scan" else _capi.KERNEL_GENERAL
-    if policy == "scan":   # the scan kernel's shapes: clauses of 1..5 literals
+    kern = {"scan": _capi.KERNEL_SCAN, "inc": _capi.KERNEL_INC, "general": _capi.KERNEL_GENERAL}[policy]
+    if policy != "general":   # the clause kernels' shapes: clauses of 1..5 literals
         cases = [c for c in cases if c["formula"] and all(1 <= len(cl) <= 5 for cl in c["formula"])]
     assert sum(c["tag"] == "configs2_n100" for c in cases) >= 48
     fs = [c["formula"] for c in cases]
@@ -348,10 +351,12 @@ def test_scan_kernel_chunk_group_tails(n, m, cap):
     for_chunks path of dpll_scan.hip no other shape reaches.  Scan kernel vs
     general kernel vs oracle, node-capped, every counter and any model."""
     batch = cnf.uniform_ksat(6, n, m, 3, seed=n + m)
-    rs = _run_policy(batch, _capi.KERNEL_SCAN, max_solutions=1, node_limit=cap, sol_cap=1)
     rg = _run_policy(batch, _capi.KERNEL_GENERAL, max_solutions=1, node_limit=cap, sol_cap=1)
-    assert (rs.status == rg.status).all()
-    assert (rs.counters[:, :7] == rg.counters[:, :7]).all()
+    ri = _run_policy(batch, _capi.KERNEL_INC, max_solutions=1, node_limit=cap, sol_cap=1)
+    rs = _run_policy(batch, _capi.KERNEL_SCAN, max_solutions=1, node_limit=cap, sol_cap=1)
+    for r in (rs, ri):
+        assert (r.status == rg.status).all()
+        assert (r.counters[:, :7] == rg.counters[:, :7]).all()
     for b in range(6):
         o = oracle.dpll(batch.instance(b), "sound", max_solutions=1, node_limit=cap, sol_cap=1)
         assert int(rs.status[b]) == o["status"]

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--lib", default=None, help="load this libsatmi build instead (experiments)")
-    ap.add_argument("--kernel", choices=("auto", "general", "scan"), default="auto")
+    ap.add_argument("--kernel", choices=("auto", "general", "scan", "inc"), default="auto")
     ap.add_argument("--diag", action="store_true", help="load libsatmi_diag.so and report per-phase clocks")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -35,7 +35,7 @@ def main():
     if a.diag:
         _capi.LIB_PATH = os.path.join(os.path.dirname(_capi.LIB_PATH), "libsatmi_diag.so")
     L = _capi.load()
-    _capi.set_kernel({"auto": _capi.KERNEL_AUTO, "general": _capi.KERNEL_GENERAL, "scan": _capi.KERNEL_SCAN}[a.kernel])
+    _capi.set_kernel({"auto": _capi.KERNEL_AUTO, "general": _capi.KERNEL_GENERAL, "scan": _capi.KERNEL_SCAN, "inc": _capi.KERNEL_INC}[a.kernel])
     B, n, k = a.per_gpu, a.n, a.k
     m = int(round(a.alpha * n))
     icb, clb, lits, nv = cnf.uniform_ksat_device(B, n, m, k, seed=a.seed, device=dev)

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU verification pass (run through gpurun from the repo root, library prebuilt):
+#   -m gpu suite (verbose log kept), smoke(), bench line, kernel trace + HBM PMC
+#   passes (tools/profile_bench.sh), SQ/LDS PMC passes (tools/profile_sq.sh).
+# Usage: bash tools/gpu_round.sh <tag> [steps...]   steps: tests smoke prof sq (default all)
+set -o pipefail
+TAG=${1:-round}
+shift || true
+STEPS=${*:-tests smoke prof sq}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for s in $STEPS; do
+  case $s in
+    tests) timeout -k 10 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+             > "$OUT/gpu_tests.log" 2>&1 || { echo "tests failed"; tail -30 "$OUT/gpu_tests.log"; exit 1; } ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+             || { echo "smoke failed"; tail -30 "$OUT/smoke.log"; exit 1; } ;;
+    prof)  bash tools/profile_bench.sh "$TAG" || { echo "profile_bench failed"; exit 1; } ;;
+    sq)    bash tools/profile_sq.sh "$TAG" || { echo "profile_sq failed"; exit 1; } ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  echo "step $s ok"
+done
+tail -3 "$OUT/gpu_tests.log" 2>/dev/null
+cat "$OUT/bench.json" 2>/dev/null

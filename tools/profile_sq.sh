@@ -7,7 +7,7 @@
 set -eo pipefail
 TAG=${1:-sq}
 B=${2:-262144}
-shift 2 || true
+shift $(( $# < 2 ? $# : 2 ))
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 ROOT=$(pwd)
