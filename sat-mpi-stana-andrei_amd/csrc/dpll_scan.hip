@@ -115,7 +115,7 @@ __device__ __forceinline__ uint32_t field(typename Pack<K>::W w, int j) {
 }
 
 struct ScanLayout {
-    uint32_t cls, lv, ts, cnt, first, trail, fvar, ftrail, scratch, occ_off, acc, pfx, bytes;
+    uint32_t cls, lv, ts, cnt, first, trail, fvar, ftrail, scratch, occ_off, bm, bytes;
     int32_t mcap, ncap, nw;   // nw: 32-clause words of the unit bitmap (incremental kernel)
 };
 
@@ -151,8 +151,8 @@ struct SLds {
     uint32_t *plist;            // scratch:  pure-literal positions (analysis), aliases snap
     // incremental kernel only
     uint16_t *occ_off;          // [2(ncap+1)+1]  start of each literal code's occurrence list in `occ`
-    uint32_t *acc;              // [nw]  unit clauses found this round, one bit per clause
-    uint2 *pfx;                 // [nw]  (bits, units before the word) of the finished bitmap
+    uint2 *bm;                  // [nw]  unit bitmap of the round: .x one bit per clause (32 clauses
+                                //       per word), .y units before the word once the round is scanned
     const uint16_t *occ;        // global: clause indices holding each literal code (distinct per clause)
 };
 
@@ -334,7 +334,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                         }
                         e = min(e, tt);
                     } else if (nf == 1u) {
-                        atomicOr(&S.acc[c >> 5], 1u << (c & 31u));
+                        atomicOr(&S.bm[c >> 5].x, 1u << (c & 31u));
                         unit = true;
                         uc = c;
                         ucode = unit_code<K>(w, x);
@@ -347,29 +347,25 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
     const int emp = __ballot(e != INT_MAX) ? wave_min_i32(e) : INT_MAX;
     *empty_at = emp;
     if (emp != INT_MAX) {   // conflict: the snapshot is not needed, only a clean bitmap
-        for (int w = ln; w < nw; w += 64) S.acc[w] = 0u;
+        for (int w = ln; w < nw; w += 64) S.bm[w].x = 0u;
         wave_sync();
         return 0;
     }
-    // prefix popcounts of the bitmap (and clear it for the next round)
+    // prefix popcounts of the bitmap
     int nu = 0;
     for (int w0 = 0; w0 < nw; w0 += 64) {
         const int w = w0 + ln;
-        uint32_t bits = 0u;
-        if (w < nw) {
-            bits = S.acc[w];
-            S.acc[w] = 0u;
-        }
+        const uint32_t bits = w < nw ? S.bm[w].x : 0u;
         const int pc = __popc(bits);
         const int in = wave_incl_scan(pc);
-        if (w < nw) S.pfx[w] = make_uint2(bits, (uint32_t)(nu + in - pc));
+        if (w < nw) S.bm[w].y = (uint32_t)(nu + in - pc);
         nu += lane63(in);
     }
     wave_sync();
     if (passes <= 1) {
         // one pass held every touched clause: each unit lane places its clause
         if (unit) {
-            const uint2 p = S.pfx[uc >> 5];
+            const uint2 p = S.bm[uc >> 5];
             const uint32_t k = p.y + (uint32_t)__popc(p.x & ((1u << (uc & 31u)) - 1u));
             S.snap[k] = (C)ucode;
             atomicMax(&S.ts[ucode >> 1], stamp(ep, k));
@@ -377,7 +373,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
     } else {
         // long batch: walk the bitmap word by word, re-deriving each unit literal
         for (int w = ln; w < nw; w += 64) {
-            const uint2 p = S.pfx[w];
+            const uint2 p = S.bm[w];
             uint32_t bits = p.x, k = p.y;
             while (bits) {
                 const uint32_t c = ((uint32_t)w << 5) | (uint32_t)__builtin_ctz(bits);
@@ -394,6 +390,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
         }
     }
     wave_sync();
+    for (int w = ln; w < nw; w += 64) S.bm[w].x = 0u;   // clean bitmap for the next round
     return nu;
 }
 
@@ -890,10 +887,9 @@ __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpl
     S.plist = (uint32_t *)(base + A.lay.scratch);
     if constexpr (INC) {
         S.occ_off = (uint16_t *)(base + A.lay.occ_off);
-        S.acc = (uint32_t *)(base + A.lay.acc);
-        S.pfx = (uint2 *)(base + A.lay.pfx);
+        S.bm = (uint2 *)(base + A.lay.bm);
         S.occ = A.occ + ((size_t)blockIdx.x * (blockDim.x >> 6) + (size_t)wave) * (size_t)A.occ_cap;
-        for (int w = lane_id(); w < A.lay.nw; w += 64) S.acc[w] = 0u;
+        for (int w = lane_id(); w < A.lay.nw; w += 64) S.bm[w].x = 0u;
         wave_sync();
     }
     span_begin(A.work_counter);
@@ -907,6 +903,56 @@ __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpl
     }
     span_end(A.work_counter);
 }
+
+// The bench shape class (K = 3, n <= 127, m <= FIXM): the incremental kernel
+// with every per-wave array static, so all LDS addresses are link-time
+// constants -- an access is `ds_* vindex offset:imm`, with no base register
+// to keep live or add (the runtime-layout kernel spends an SGPR and a VALU
+// add per access).  5,108 B of LDS per wave at FIXM = 448: 32 waves per CU.
+constexpr int FIX_NCAP = 127;
+template <int FIXM>
+__global__ void __launch_bounds__(64, SATMI_SCAN_WAVES_PER_SIMD) dpll_fixed_kernel(ScanArgs A) {
+    static_assert(FIXM % 64 == 0, "whole 64-clause chunks");
+    __shared__ __attribute__((aligned(16))) uint32_t cls_s[FIXM];
+    __shared__ __attribute__((aligned(16))) uint8_t lv_s[2 * (FIX_NCAP + 1)];
+    __shared__ __attribute__((aligned(16))) uint32_t ts_s[FIX_NCAP + 1], cnt_s[FIX_NCAP + 1], first_s[FIX_NCAP + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t trail_s[FIX_NCAP + 1], fvar_s[FIX_NCAP + 1],
+        ftrail_s[FIX_NCAP + 1];
+    // snapshot (<= FIXM + 1 byte codes) / pure-literal positions (<= 128 words)
+    __shared__ __attribute__((aligned(16))) uint32_t scratch_s[(FIXM + 4) / 4 > FIX_NCAP + 1 ? (FIXM + 4) / 4
+                                                                                             : FIX_NCAP + 1];
+    __shared__ __attribute__((aligned(16))) uint16_t occ_off_s[2 * (FIX_NCAP + 1) + 2];
+    __shared__ __attribute__((aligned(16))) uint2 bm_s[FIXM / 32];
+    SLds<3, uint8_t> S;
+    S.cls = cls_s;
+    S.lv = lv_s;
+    S.ts = ts_s;
+    S.cnt = cnt_s;
+    S.first = first_s;
+    S.trail = trail_s;
+    S.fvar = fvar_s;
+    S.ftrail = ftrail_s;
+    S.snap = (uint8_t *)scratch_s;
+    S.plist = scratch_s;
+    S.occ_off = occ_off_s;
+    S.bm = bm_s;
+    S.occ = A.occ + (size_t)blockIdx.x * (size_t)A.occ_cap;
+    for (int w = lane_id(); w < FIXM / 32; w += 64) S.bm[w].x = 0u;
+    wave_sync();
+    span_begin(A.work_counter);
+    for (;;) {
+        uint32_t b = 0;
+        if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
+        b = uniform_u32(b);
+        if (b >= (uint32_t)A.num_instances) break;
+        solve_instance<3, true, uint8_t>(A, S, (int)b);
+        wave_sync();
+    }
+    span_end(A.work_counter);
+}
+constexpr int FIX_MCAP = 448;   // configs[1] (n=50, m=213) and configs[2] (n=100, m=426)
+constexpr uint32_t FIX_LDS_BYTES = 4 * FIX_MCAP + 2 * (FIX_NCAP + 1) + 3 * 4 * (FIX_NCAP + 1) + 3 * (FIX_NCAP + 1) +
+                                   4 * (FIX_NCAP + 1) + 2 * (2 * (FIX_NCAP + 1) + 2) + 8 * (FIX_MCAP / 32);
 
 // Static literal-state size class of the one-wave kernel: 2(n+1) bytes rounded
 // up to 256 (n <= 127) or to the packing's variable limit.
@@ -942,8 +988,7 @@ bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, bool inc, u
     lay->ftrail = o;  o = align16(o + cb * N);
     lay->scratch = o; o = align16(o + std::max(cb * M, 4 * N));
     lay->occ_off = o; o = align16(o + (inc ? 2 * (2 * N + 1) : 0u));
-    lay->acc = o;     o = align16(o + (inc ? 4 * NW : 0u));
-    lay->pfx = o;     o = align16(o + (inc ? 8 * NW : 0u));
+    lay->bm = o;      o = align16(o + (inc ? 8 * NW : 0u));
     lay->bytes = o;
     lay->mcap = max_clauses;
     lay->ncap = max_vars;
@@ -964,14 +1009,35 @@ const void *scan_fn(int K, int lvs, bool inc) { return inc ? scan_fn<true>(K, lv
 
 struct ScanPlan {
     int waves_per_wg = 1, wg_per_cu = 1, lvs = 0;
+    bool fixed = false;   // dpll_fixed_kernel<FIX_MCAP> (static layout)
     ScanLayout lay;
 };
+
+bool fixed_class(int K, int max_vars, int max_clauses, bool inc) {
+    return inc && K == 3 && max_vars <= FIX_NCAP && max_clauses <= FIX_MCAP;
+}
 
 // Launch shape: the workgroup size that keeps the most waves resident under
 // LDS (<= 32 waves per CU) and the kernel's register budget
 // (hipOccupancyMaxActiveBlocksPerMultiprocessor); one-wave workgroups (the
 // cheaper gather addressing) whenever they reach the same residency.
 int scan_plan(int K, int max_vars, int max_clauses, bool inc, ScanPlan *P) {
+    if (fixed_class(K, max_vars, max_clauses, inc)) {
+        const void *fn = (const void *)dpll_fixed_kernel<FIX_MCAP>;
+        int occ = 0, wgs = 32;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64, 0) == hipSuccess && occ > 0)
+            wgs = std::min(wgs, occ);
+        P->fixed = true;
+        P->waves_per_wg = 1;
+        P->wg_per_cu = wgs;
+        P->lvs = 0;
+        P->lay = ScanLayout{};
+        P->lay.mcap = FIX_MCAP;
+        P->lay.ncap = FIX_NCAP;
+        P->lay.nw = FIX_MCAP / 32;
+        P->lay.bytes = 0;
+        return SATMI_OK;
+    }
     int best = 0;
     for (int wpg : {1, 4, 2}) {
         const int lvs = wpg == 1 ? lv_static_class(K, max_vars) : 0;
@@ -1037,7 +1103,7 @@ int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, bool i
     const int rc = scan_plan(K, max_vars, max_clauses, inc, &P);
     if (rc) return rc;
     *waves_per_cu = P.waves_per_wg * P.wg_per_cu;
-    if (lds_per_wave) *lds_per_wave = P.lay.bytes + (uint32_t)P.lvs;
+    if (lds_per_wave) *lds_per_wave = P.fixed ? FIX_LDS_BYTES : P.lay.bytes + (uint32_t)P.lvs;
     return SATMI_OK;
 }
 
@@ -1088,7 +1154,8 @@ int dpll_scan_launch(const ScanLaunch &L) {
         }
     }
     const dim3 g(grid), blk(64 * waves_per_wg);
-    if (L.inc) launch_kernel<true>(K, P.lvs, g, blk, wg_lds, L.stream, A);
+    if (P.fixed) hipLaunchKernelGGL((dpll_fixed_kernel<FIX_MCAP>), g, blk, 0, L.stream, A);
+    else if (L.inc) launch_kernel<true>(K, P.lvs, g, blk, wg_lds, L.stream, A);
     else launch_kernel<false>(K, P.lvs, g, blk, wg_lds, L.stream, A);
     SATMI_HIP(hipGetLastError());
     return SATMI_OK;

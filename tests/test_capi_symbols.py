@@ -66,8 +66,18 @@ def test_scan_kernel_eligibility_query():
     # in a 256-B static array instead of the image's 2(n+1) = 202 B (+ alignment),
     # and (n <= 127) byte-wide trail / frames / snapshot: 3 x (208 - 112) + (864 - 432)
     assert kern == _capi.KERNEL_SCAN and s100 - 208 + 256 - 3 * 96 - 432 == lds
-    # + occurrence-list offsets (2(2n+3) B) and the unit bitmap / its prefixes (14 x 12 B)
-    assert lds_inc == lds + 416 + 64 + 112
+    # the bench class (K=3, n <= 127, m <= 448) runs the static-layout incremental
+    # kernel: 5,108 B per wave whatever the instance size, 32 waves per CU
+    assert lds_inc == 5108 and _capi.plan(50, 213, 639, 3)[1] == 5108
+    # beyond it, the runtime layout: + occurrence-list offsets (2(2n+3) B) and the
+    # unit bitmap with its prefixes (8 B per 32 clauses)
+    kern, lds_big, _ = _capi.plan(130, 426, 1278, 3)
+    _capi.set_kernel(_capi.KERNEL_SCAN)
+    try:
+        lds_big_scan = _capi.plan(130, 426, 1278, 3)[1]
+    finally:
+        _capi.set_kernel(_capi.KERNEL_AUTO)
+    assert kern == _capi.KERNEL_INC and lds_big == lds_big_scan + 528 + 112
     _capi.set_kernel(_capi.KERNEL_GENERAL)
     try:
         assert _capi.plan(100, 426, 1278, 3)[0] == _capi.KERNEL_GENERAL
