@@ -284,10 +284,89 @@ __device__ int scan_units(const SLds<K, C> &S, int mpad, uint32_t ep, uint32_t b
 // reached twice counted once.  Emptied clauses are found among the same
 // touched clauses (an emptied clause lost its last literal in this batch).
 // Same results as scan_units, bit for bit.
+// Emptied-clause search of one touched clause (REF.py:161-162): the snapshot
+// index in batch epoch `bep` of its latest-stamped literal, -1 if none.
+template <int K, typename C>
+__device__ __forceinline__ int emptier(const SLds<K, C> &S, typename Pack<K>::W w, uint32_t bep) {
+    int tt = -1;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const uint32_t code = field<K>(w, j);
+        const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : 0u;
+        if ((st >> 16) == bep) tt = max(tt, (int)stamp_index(st));
+    }
+    return tt;
+}
+
+// Unit clauses in a round whose touched clauses fit one wave step and that
+// found at most this many of them: ranked in clause order by register
+// comparisons (no bitmap round trips through LDS).
+constexpr int FAST_UNITS = 8;
+
 template <int K, typename C>
 __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t ep, uint32_t bep, int *empty_at) {
     using W = typename Pack<K>::W;
     const int ln = lane_id();
+    if (tl - rs <= 64) {
+        // lane b: the b-th batch literal's negation and its occurrence list
+        int ob = 0, len = 0;
+        if (ln < tl - rs) {
+            const uint32_t x = (uint32_t)S.trail[rs + ln] ^ 1u;
+            ob = S.occ_off[x];
+            len = (int)S.occ_off[x + 1] - ob;
+        }
+        const int incl = wave_incl_scan(len);
+        const int excl = incl - len;
+        const int delta = ob - excl;
+        const int total = lane63(incl);
+        if (total <= 64) {
+            // one touched clause per lane
+            int d = 0;
+            for (int b = 0; b < tl - rs; ++b) {
+                const int eb = __builtin_amdgcn_readlane(excl, b);
+                const int db = __builtin_amdgcn_readlane(delta, b);
+                d = ln >= eb ? db : d;
+            }
+            const bool valid = ln < total;
+            const uint32_t c = S.occ[valid ? d + ln : 0];
+            const W w = S.cls[c];
+            uint32_t x[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = S.lv[field<K>(w, j)];
+            const uint32_t s = clause_sum<K>(x);
+            const bool open = valid && !sum_true(s);
+            const uint32_t nf = sum_nfree(s);
+            const bool empty = open && nf == 0u;
+            if (__builtin_expect(__ballot(empty) != 0ull, 0)) {
+                const int e = empty ? emptier<K>(S, w, bep) : INT_MAX;
+                *empty_at = wave_min_i32(e);
+                return 0;
+            }
+            *empty_at = INT_MAX;
+            const bool unit = open && nf == 1u;
+            const uint64_t um = __ballot(unit);
+            const int nun = __popcll(um);
+            if (nun <= FAST_UNITS) {
+                // a clause reached from two batch literals is one snapshot entry
+                bool dup = false;
+                for (uint64_t r = um; r; r &= r - 1) {
+                    const int u = __builtin_ctzll(r);
+                    dup |= u < ln && (uint32_t)__builtin_amdgcn_readlane((int)c, u) == c;
+                }
+                const uint64_t dm = __ballot(unit && !dup);
+                int rank = 0;
+                for (uint64_t r = dm; r; r &= r - 1)
+                    rank += (uint32_t)__builtin_amdgcn_readlane((int)c, __builtin_ctzll(r)) < c ? 1 : 0;
+                if (unit && !dup) {
+                    const uint32_t code = unit_code<K>(w, x);
+                    S.snap[rank] = (C)code;
+                    atomicMax(&S.ts[code >> 1], stamp(ep, (uint32_t)rank));
+                }
+                wave_sync();
+                return __popcll(dm);
+            }
+        }
+    }
     int e = INT_MAX;
     int passes = 0;
     bool unit = false;          // this lane found a unit clause (valid when one pass covered all touched clauses)
@@ -325,14 +404,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 if (!sum_true(s)) {
                     const uint32_t nf = sum_nfree(s);
                     if (nf == 0u) {   // emptied in this batch: by its latest-stamped literal
-                        int tt = -1;
-#pragma unroll
-                        for (int j = 0; j < K; ++j) {
-                            const uint32_t code = field<K>(w, j);
-                            const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : 0u;
-                            if ((st >> 16) == bep) tt = max(tt, (int)stamp_index(st));
-                        }
-                        e = min(e, tt);
+                        e = min(e, emptier<K>(S, w, bep));
                     } else if (nf == 1u) {
                         atomicOr(&S.bm[c >> 5].x, 1u << (c & 31u));
                         unit = true;

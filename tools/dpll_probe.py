@@ -27,12 +27,12 @@ def main():
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--lib", default=None, help="load this libsatmi build instead (experiments)")
     ap.add_argument("--kernel", choices=("auto", "general", "scan", "inc"), default="auto")
-    ap.add_argument("--diag", action="store_true", help="load libsatmi_diag.so and report per-phase clocks")
+    ap.add_argument("--diag", action="store_true", help="load libsatmi_diag.so (or --lib, a diag build) and report per-phase clocks")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     if a.lib:
         _capi.LIB_PATH = os.path.abspath(a.lib)
-    if a.diag:
+    if a.diag and not a.lib:
         _capi.LIB_PATH = os.path.join(os.path.dirname(_capi.LIB_PATH), "libsatmi_diag.so")
     L = _capi.load()
     _capi.set_kernel({"auto": _capi.KERNEL_AUTO, "general": _capi.KERNEL_GENERAL, "scan": _capi.KERNEL_SCAN, "inc": _capi.KERNEL_INC}[a.kernel])
@@ -75,7 +75,7 @@ def main():
                "sat": int((c[:, 5] > 0).sum())}
         if a.diag:
             names = (("stage", "assign", "units", "conflict", "counts", "choose", "pure", "other")
-                     if kern == _capi.KERNEL_SCAN else
+                     if kern in (_capi.KERNEL_SCAN, _capi.KERNEL_INC) else
                      ("stage", "assign", "apply", "collect", "analyze", "pure", "backtrack", "other"))
             ph = root[:, :16].cpu().contiguous().view(torch.int64)[:, :8].double().sum(0)
             nodes = float(c[:, 0].sum())
