@@ -157,6 +157,36 @@ def load_pmc(workload_key):
         return None
 
 
+def issue_roofline(preset, per_gpu, kernel_ms):
+    """The DPLL kernel's binding resource is inside the CU: issue-pipe fractions
+    from the SQ counter passes kept in profiles/sq_issue.json (tools/sq_roofline.py:
+    wave-instructions / LDS-array cycles per launch of this exact workload) over
+    this run's live kernel time at the profiled effective clock.  Peaks: VALU 0.5
+    wave-instructions / cycle / SIMD, SALU 1 / cycle / CU, LDS array 1 cycle /
+    cycle / CU.  `stale` if the kernel source changed since the profile."""
+    import hashlib
+    try:
+        with open(os.path.join(ROOT, "profiles", "sq_issue.json")) as fh:
+            e = json.load(fh).get(f"{preset}_B{per_gpu}")
+        with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", "dpll_scan.hip"), "rb") as fh:
+            sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    except (OSError, ValueError):
+        return None
+    if not e:
+        return None
+    cyc = e["effective_clock_hz"] * kernel_ms * 1e-3
+    pipes = {"valu": (e["valu_insts"], 1024 * 0.5 * cyc, "wave-instr"),
+             "salu": (e["salu_insts"], 256 * cyc, "instr"),
+             "lds": (e["lds_array_cycles"], 256 * cyc, "array-cycles")}
+    fr = {k: a / p for k, (a, p, _) in pipes.items()}
+    bound = max(fr, key=fr.get)
+    a, p, unit = pipes[bound]
+    return {"bound": bound, "achieved": a / (kernel_ms * 1e-3), "peak": p / (kernel_ms * 1e-3),
+            "unit": unit + "/s", "frac": fr[bound], "fracs": fr,
+            "lds_bank_conflict_share": e["lds_bank_conflict_cycles"] / e["lds_array_cycles"],
+            "clock_hz": e["effective_clock_hz"], "source": e["source"], "stale": e["kernel_src_sha256_16"] != sha}
+
+
 def saturation_main(args):
     """configs[3]: Davis-Putnam / resolution saturation of a pigeonhole formula.
     A step = one full satmi_dp_host / satmi_resolution_host call (host arrays in,
@@ -396,6 +426,7 @@ def main():
         "hbm_gbs": achieved,
         "wave_utilisation": util,
         "roofline": roof,
+        "roofline_issue": issue_roofline(args.workload, B, kernel_ms),
     }
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and not args.profile_steps:
