@@ -116,7 +116,7 @@ int satmi_dpll_batch_host(int num_instances, const int32_t *h_inst_clause_begin,
  * Resolution saturation, replaces resolution_solver (REF.py:63-95) for one
  * clause set (CSR host arrays: clause c = lits[clause_off[c] .. clause_off[c+1])).
  * Clauses are variable bitsets in HBM; each pass resolves all pairs on the GPU
- * (tautologies filtered), dedups by sort + merge against the sorted `seen` set.
+ * (tautologies filtered), dedups through a hash table over every clause key.
  *   max_passes / clause_limit / time_limit_s   <= 0: unlimited
  *   *result   1 = True (no new clause derivable), 0 = False (empty resolvent),
  *             -1 = a limit stopped the saturation
@@ -130,6 +130,10 @@ int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, const int32
                           int32_t *h_result, int32_t *h_passes, int64_t *h_pass_new, int pass_cap,
                           int32_t *h_rec_lits, int64_t rec_lit_cap, int64_t *h_rec_clause_off,
                           int64_t rec_clause_cap, int64_t *h_rec_pass_off, int rec_pass_cap);
+
+/* Test knob: the pair kernel's first candidate append slot (default 0), so a
+ * small pass exercises the slot arithmetic past 2^31 / 2^32 candidates. */
+int satmi_resolution_debug_slot_base(int64_t base);
 
 /*
  * Davis-Putnam elimination, replaces davis_putnam_solver (REF.py:98-130) for one

@@ -1,7 +1,7 @@
 // prims.h -- device-wide building blocks for the clause-set kernels (gfx950):
-// exclusive scan of int64 counts, stable merge sort of an index array under a
-// key comparator, rank-merge of two sorted key arrays.  All launches go on the
-// caller's stream; no host synchronisation happens here.
+// grid sizing and the exclusive scan of int64 flags / counts (compaction in
+// resolution.hip and dp.hip).  All launches go on the caller's stream; no host
+// synchronisation happens here.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -13,73 +13,11 @@ namespace {   // internal linkage: every TU that includes this gets its own kern
 
 constexpr int PRIM_BLOCK = 256;
 
-// ---------------------------------------------------------------- multiword keys
-// A clause key is K uint64 words: positive-literal bitset words then negative
-// ones over the formula's dense variable index.  Order: lexicographic.
-struct KeyView {
-    const uint64_t *w;
-    int K;
-    __device__ __forceinline__ const uint64_t *at(int64_t i) const { return w + i * K; }
-};
-
-__device__ __forceinline__ int key_cmp(const uint64_t *a, const uint64_t *b, int K) {
-    for (int k = 0; k < K; ++k) {
-        if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
-    }
-    return 0;
-}
-
-// number of elements of sorted idx[lo, hi) whose key is < x (strict) or <= x
-template <bool UPPER>
-__device__ int64_t rank_in(const KeyView &kv, const int64_t *idx, int64_t lo, int64_t hi, const uint64_t *x) {
-    int64_t a = lo, b = hi;
-    while (a < b) {
-        const int64_t mid = (a + b) >> 1;
-        const int c = key_cmp(kv.at(idx ? idx[mid] : mid), x, kv.K);
-        if (c < 0 || (UPPER && c == 0)) a = mid + 1;
-        else b = mid;
-    }
-    return a - lo;
-}
-
-// one pass of a stable bottom-up merge sort of idx by key: runs of `width`
-__global__ void merge_pass_kernel(KeyView kv, const int64_t *in, int64_t *out, int64_t n, int64_t width) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t a0 = (i / (2 * width)) * (2 * width);
-        const int64_t a1 = min(a0 + width, n), b1 = min(a0 + 2 * width, n);
-        const int64_t x = in[i];
-        int64_t pos;
-        if (i < a1) pos = i + rank_in<false>(kv, in, a1, b1, kv.at(x));          // A before equal B
-        else pos = a0 + (i - a1) + rank_in<true>(kv, in, a0, a1, kv.at(x));
-        out[pos] = x;
-    }
-}
-
-__global__ void iota_kernel(int64_t *a, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        a[i] = i;
-}
-
 static inline int grid_for(int64_t n, int block = PRIM_BLOCK) {
     int64_t g = (n + block - 1) / block;
     if (g < 1) g = 1;
     if (g > 65536) g = 65536;
     return (int)g;
-}
-
-// Sort indices 0..n-1 by key; result in *result (== a or tmp).  a, tmp: n int64 each.
-static inline int sort_indices(KeyView kv, int64_t n, int64_t *a, int64_t *tmp, int64_t **result, hipStream_t s) {
-    hipLaunchKernelGGL(iota_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, a, n);
-    int64_t *src = a, *dst = tmp;
-    for (int64_t w = 1; w < n; w *= 2) {
-        hipLaunchKernelGGL(merge_pass_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, kv, src, dst, n, w);
-        int64_t *t = src;
-        src = dst;
-        dst = t;
-    }
-    *result = src;
-    SATMI_HIP(hipGetLastError());
-    return SATMI_OK;
 }
 
 // ---------------------------------------------------------------- exclusive scan

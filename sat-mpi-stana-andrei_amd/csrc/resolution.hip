@@ -14,9 +14,12 @@
 //     (Pi|Pj, Ni|Nj) minus that variable, a tautology iff its two halves meet,
 //     empty iff both are zero.  Candidates are appended with one atomic per
 //     wavefront (ballot + popcount);
-//   * sort-based dedup: stable merge sort of the candidate indices by key,
-//     keep the first of every run that is absent from `seen` (binary search in
-//     the sorted `seen` array), scan + scatter, then rank-merge into `seen`;
+//   * hash dedup: one open-addressing table per pass over every clause key
+//     (the reference's `seen`), then every candidate claims its key's slot
+//     run with a 64-bit CAS; the claimers are the pass's new clauses,
+//     compacted (flag scan) and appended to the clause array;
+//   * a pass's pairs run in launches of PAIR_CHUNK, the deadline checked
+//     between them, so a long pass ends as a timeout (REF.py:417-437);
 //   * semi-naive passes: pairs whose newer clause was added in the previous pass
 //     (all pairs in pass 1) -- every older pair was resolved in an earlier pass
 //     and its resolvents are already in `seen`, so the new set is identical.
@@ -52,14 +55,18 @@ __device__ __forceinline__ int64_t tri(int64_t j) { return j * (j - 1) / 2; }   
 
 // Pairs (i < j) with j in [jlo, N).  WRITE=false: count candidates; WRITE=true:
 // append them to cand (slots from *count, which must start at 0).
+// Pairs are numbered q = tri(j) + i over the whole pass; this launch takes
+// q in [tri(jlo) + p_begin, tri(jlo) + p_begin + npairs) (a chunk of the pass).
+// WRITE: candidate slot k (from *count, which starts at `slot_base`) goes to
+// cand[k - slot_base].
 template <bool WRITE>
-__global__ void __launch_bounds__(256) res_pairs_kernel(const uint64_t *keys, int W, int64_t jlo, int64_t npairs,
-                                                        unsigned long long *count, int *empty_found,
-                                                        uint64_t *cand, int64_t cand_cap) {
+__global__ void __launch_bounds__(256) res_pairs_kernel(const uint64_t *keys, int W, int64_t jlo, int64_t p_begin,
+                                                        int64_t npairs, unsigned long long *count, int *empty_found,
+                                                        uint64_t *cand, int64_t cand_cap, int64_t slot_base) {
     const int K = 2 * W;
     const int ln = lane_id();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t base = tri(jlo);
+    const int64_t base = tri(jlo) + p_begin;
     for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x; p0 < npairs; p0 += stride) {
         const int64_t p = p0 + threadIdx.x;
         bool is_cand = false;
@@ -108,7 +115,7 @@ __global__ void __launch_bounds__(256) res_pairs_kernel(const uint64_t *keys, in
         slot0 = (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)slot0) |
                 ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(slot0 >> 32)) << 32);
         if (WRITE && is_cand) {
-            const int64_t slot = (int64_t)slot0 + __popcll(m & lanemask_lt());
+            const int64_t slot = (int64_t)slot0 + __popcll(m & lanemask_lt()) - slot_base;
             if (slot >= 0 && slot < cand_cap) {
                 const uint64_t *a = keys + i * K, *b = keys + j * K;
                 uint64_t *r = cand + slot * K;
@@ -126,44 +133,74 @@ __global__ void __launch_bounds__(256) res_pairs_kernel(const uint64_t *keys, in
     }
 }
 
-// flag[t] = sorted candidate t is the first of its run and not in seen
-__global__ void res_unique_kernel(KeyView cand, const int64_t *perm, int64_t n, KeyView seen, int64_t nseen,
-                                  int64_t *flag) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t *x = cand.at(perm[t]);
-        bool keep = t == 0 || key_cmp(cand.at(perm[t - 1]), x, cand.K) != 0;
-        if (keep && nseen > 0) {
-            const int64_t r = rank_in<false>(seen, nullptr, 0, nseen, x);
-            if (r < nseen && key_cmp(seen.at(r), x, seen.K) == 0) keep = false;
+// ---- dedup by hashing: one open-addressing table per pass over every clause
+// key (the reference's `seen`, REF.py:65/94) and every candidate.  A candidate
+// is new iff it is the first to claim its key's slot run: neither an old
+// clause nor an earlier-claiming equal candidate holds the key.  Which of
+// several equal candidates wins is left to the hardware; the *set* of new
+// keys -- all REF.py's pass depends on -- is not.  Expected O(1) probes per
+// key at load factor <= 1/2, against the O(n log^2 n) of a comparison sort.
+constexpr uint64_t HT_EMPTY = ~0ull;
+constexpr uint64_t CAND_BIT = 1ull << 62;   // table value: candidate (append slot) vs clause index
+
+struct KeySrc {
+    const uint64_t *clauses, *cand;
+    int64_t base;   // append slot of cand[0]
+    int K;
+    __device__ __forceinline__ const uint64_t *at(uint64_t v) const {
+        return (v & CAND_BIT) ? cand + ((int64_t)(v & ~CAND_BIT) - base) * K : clauses + (int64_t)v * K;
+    }
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t key_hash(const uint64_t *x, int K) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int w = 0; w < K; ++w) h = mix64(h ^ x[w]) + (uint64_t)w;
+    return h;
+}
+
+__device__ __forceinline__ bool key_eq(const uint64_t *a, const uint64_t *b, int K) {
+    for (int w = 0; w < K; ++w)
+        if (a[w] != b[w]) return false;
+    return true;
+}
+
+// Claim a slot for value v (key x).  Returns true with *slot if x was absent.
+__device__ bool ht_insert(uint64_t *table, uint64_t mask, const KeySrc &S, uint64_t v, const uint64_t *x) {
+    uint64_t s = key_hash(x, S.K) & mask;
+    for (;;) {
+        uint64_t cur = __hip_atomic_load(table + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == HT_EMPTY) {
+            cur = atomicCAS((unsigned long long *)(table + s), (unsigned long long)HT_EMPTY, (unsigned long long)v);
+            if (cur == HT_EMPTY) return true;
         }
-        flag[t] = keep ? 1 : 0;
+        if (key_eq(S.at(cur), x, S.K)) return false;
+        s = (s + 1) & mask;
     }
 }
 
-__global__ void res_scatter_kernel(KeyView cand, const int64_t *perm, const int64_t *flag, const int64_t *pos,
-                                   int64_t n, uint64_t *out) {
+__global__ void ht_clauses_kernel(uint64_t *table, uint64_t mask, KeySrc S, int64_t ncl) {
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncl; c += (int64_t)gridDim.x * blockDim.x)
+        (void)ht_insert(table, mask, S, (uint64_t)c, S.clauses + c * S.K);
+}
+
+// flag[t] = candidate t claimed its key (new in this pass)
+__global__ void ht_cand_kernel(uint64_t *table, uint64_t mask, KeySrc S, int64_t n, int64_t *flag) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+        flag[t] = ht_insert(table, mask, S, CAND_BIT | (uint64_t)(S.base + t), S.cand + t * S.K) ? 1 : 0;
+}
+
+// clauses.extend(new): the claimed candidates, in append order, after clause ncl
+__global__ void res_append_kernel(const uint64_t *cand, const int64_t *flag, const int64_t *pos, int64_t n, int K,
+                                  uint64_t *dst) {
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
         if (!flag[t]) continue;
-        const uint64_t *x = cand.at(perm[t]);
-        uint64_t *o = out + pos[t] * cand.K;
-        for (int w = 0; w < cand.K; ++w) o[w] = x[w];
-    }
-}
-
-// merge two sorted, disjoint key arrays A (na) and B (nb) into out
-__global__ void res_merge_kernel(KeyView A, int64_t na, KeyView B, int64_t nb, uint64_t *out) {
-    const int K = A.K;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < na + nb; t += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t *x;
-        int64_t pos;
-        if (t < na) {
-            x = A.at(t);
-            pos = t + rank_in<false>(B, nullptr, 0, nb, x);
-        } else {
-            x = B.at(t - na);
-            pos = (t - na) + rank_in<false>(A, nullptr, 0, na, x);
-        }
-        for (int w = 0; w < K; ++w) out[pos * K + w] = x[w];
+        for (int w = 0; w < K; ++w) dst[pos[t] * K + w] = cand[t * K + w];
     }
 }
 
@@ -196,43 +233,62 @@ struct DevBuf {
         if (_rc != SATMI_OK) return _rc; \
     } while (0)
 
-// Sort + dedup `n` candidate keys against the sorted `seen` (nseen); writes the
-// new sorted keys to out_new and returns their count through *nnew.
-struct Dedup {
-    DevBuf perm_a, perm_b, flag, pos, tiles, grand;
-    int run(const uint64_t *cand, int64_t n, const uint64_t *seen, int64_t nseen, int K, DevBuf &out_new,
+// One pass's dedup (see ht_insert): a fresh table over every clause key, then
+// the candidates' claims; flag / pos (exclusive scan) give the new keys in
+// append order, *nnew their count.
+struct HashDedup {
+    DevBuf table, flag, pos, tiles, grand;
+    static uint64_t table_slots(int64_t keys) {
+        uint64_t cap = 64;
+        while (cap < 2 * (uint64_t)keys) cap <<= 1;
+        return cap;
+    }
+    int run(const uint64_t *clauses, int64_t ncl, const uint64_t *cand, int64_t n, int64_t slot_base, int K,
             int64_t *nnew, hipStream_t s) {
         *nnew = 0;
         if (n == 0) return SATMI_OK;
-        SATMI_TRY(perm_a.reserve(8 * n));
-        SATMI_TRY(perm_b.reserve(8 * n));
-        SATMI_TRY(flag.reserve(8 * n));
-        SATMI_TRY(pos.reserve(8 * n));
-        SATMI_TRY(tiles.reserve(8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 1)));
+        const uint64_t cap = table_slots(ncl + n);
+        SATMI_TRY(table.reserve(8 * cap));
+        SATMI_TRY(flag.reserve(8 * (size_t)n));
+        SATMI_TRY(pos.reserve(8 * (size_t)n));
+        SATMI_TRY(tiles.reserve(8 * (size_t)((n + SCAN_TILE - 1) / SCAN_TILE + 1)));
         SATMI_TRY(grand.reserve(8));
-        KeyView kc{cand, K}, ks{seen, K};
-        int64_t *perm = nullptr;
-        SATMI_TRY(sort_indices(kc, n, perm_a.as<int64_t>(), perm_b.as<int64_t>(), &perm, s));
-        hipLaunchKernelGGL(res_unique_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, kc, perm, n, ks, nseen,
-                           flag.as<int64_t>());
+        SATMI_HIP(hipMemsetAsync(table.p, 0xFF, 8 * cap, s));   // HT_EMPTY
+        const KeySrc S{clauses, cand, slot_base, K};
+        if (ncl > 0)
+            hipLaunchKernelGGL(ht_clauses_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(),
+                               cap - 1, S, ncl);
+        hipLaunchKernelGGL(ht_cand_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(), cap - 1,
+                           S, n, flag.as<int64_t>());
+        SATMI_HIP(hipGetLastError());
         SATMI_TRY(exclusive_scan(flag.as<int64_t>(), pos.as<int64_t>(), n, tiles.as<int64_t>(),
                                  grand.as<int64_t>(), s));
         SATMI_HIP(hipMemcpyAsync(nnew, grand.p, 8, hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
-        if (*nnew == 0) return SATMI_OK;
-        SATMI_TRY(out_new.reserve(8 * (size_t)*nnew * K));
-        hipLaunchKernelGGL(res_scatter_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, kc, perm,
-                           flag.as<int64_t>(), pos.as<int64_t>(), n, out_new.as<uint64_t>());
-        SATMI_HIP(hipGetLastError());
         return SATMI_OK;
     }
 };
+
+// pairs per launch: a pass is cut into launches of this many pairs so that the
+// deadline is checked inside a long pass (REF.py:417-437's timeout)
+constexpr int64_t PAIR_CHUNK = 1ll << 30;
+
+int64_t g_slot_base = 0;   // test knob: first append slot of the pair kernel
 
 }  // namespace
 
 }  // namespace satmi
 
 using namespace satmi;
+
+extern "C" int satmi_resolution_debug_slot_base(int64_t base) {
+    if (base < 0 || base > (1ll << 61)) {
+        set_error("satmi_resolution_debug_slot_base: base out of range");
+        return SATMI_ERR_ARG;
+    }
+    g_slot_base = base;
+    return SATMI_OK;
+}
 
 extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_lits,
                                      int64_t max_passes, int64_t clause_limit, double time_limit_s,
@@ -244,6 +300,10 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
         return SATMI_ERR_ARG;
     }
     const auto t_start = std::chrono::steady_clock::now();
+    const auto expired = [&]() {
+        return time_limit_s > 0 &&
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > time_limit_s;
+    };
     *h_result = -1;
     *h_passes = 0;
     if (h_rec_pass_off && rec_pass_cap > 0) h_rec_pass_off[0] = 0;
@@ -268,9 +328,10 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
     const int V = (int)dense2var.size();
     const int W = std::max(1, (V + 63) / 64);
     const int K = 2 * W;
+    const int64_t slot_base = g_slot_base;
     hipStream_t s = nullptr;
 
-    DevBuf d_off, d_lits, d_map, clauses, seen, seen2, cand, newk, counters;
+    DevBuf d_off, d_lits, d_map, clauses, cand, counters;
     SATMI_TRY(d_off.reserve(4 * (size_t)(nclauses + 1)));
     SATMI_TRY(d_lits.reserve(4 * (size_t)std::max<int64_t>(L, 1)));
     SATMI_TRY(d_map.reserve(4 * (size_t)(maxvar + 1)));
@@ -286,33 +347,55 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
                            clauses.as<uint64_t>());
         SATMI_HIP(hipGetLastError());
     }
-    // seen = {frozenset(c) for c in clauses}  (REF.py:65): sorted unique input keys
-    Dedup dd;
-    int64_t nseen = 0;
-    SATMI_TRY(dd.run(clauses.as<uint64_t>(), ncl, nullptr, 0, K, seen, &nseen, s));
+    HashDedup dd;
+    unsigned long long *d_count = counters.as<unsigned long long>();
+    int *d_empty = (int *)(counters.as<char>() + 8);
+    // one sweep of the pass's pairs (count or write), a launch per PAIR_CHUNK;
+    // false if the deadline passed between two launches
+    const auto sweep = [&](bool write, int64_t npairs, int64_t jlo, int64_t ncand, int *rc) {
+        *rc = SATMI_OK;
+        for (int64_t p = 0; p < npairs; p += PAIR_CHUNK) {
+            if (p > 0) {
+                if (hipStreamSynchronize(s) != hipSuccess) {
+                    *rc = hip_fail(hipGetLastError(), "resolution pair sweep");
+                    return false;
+                }
+                if (expired()) return false;
+            }
+            const int64_t np = std::min(PAIR_CHUNK, npairs - p);
+            if (write)
+                hipLaunchKernelGGL(res_pairs_kernel<true>, dim3(grid_for(np)), dim3(256), 0, s,
+                                   clauses.as<uint64_t>(), W, jlo, p, np, d_count, d_empty, cand.as<uint64_t>(),
+                                   ncand, slot_base);
+            else
+                hipLaunchKernelGGL(res_pairs_kernel<false>, dim3(grid_for(np)), dim3(256), 0, s,
+                                   clauses.as<uint64_t>(), W, jlo, p, np, d_count, d_empty, nullptr, (int64_t)0,
+                                   (int64_t)0);
+            if (hipGetLastError() != hipSuccess) {
+                *rc = hip_fail(hipErrorLaunchFailure, "res_pairs_kernel");
+                return false;
+            }
+        }
+        return true;
+    };
 
     int64_t jlo = 0, rec_clauses = 0, rec_lits = 0;
     int passes = 0;
     std::vector<uint64_t> hkeys;
     for (;;) {
         if (max_passes > 0 && passes >= max_passes) break;
-        if (time_limit_s > 0 &&
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > time_limit_s)
-            break;
+        if (expired()) break;
         const int64_t npairs = (ncl * (ncl - 1) - jlo * (jlo - 1)) / 2;
         struct {
             unsigned long long count;
             int empty;
             int pad;
         } hc{0, 0, 0};
+        int rc = SATMI_OK;
         SATMI_HIP(hipMemsetAsync(counters.p, 0, 16, s));
-        unsigned long long *d_count = counters.as<unsigned long long>();
-        int *d_empty = (int *)(counters.as<char>() + 8);
-        const int grid = grid_for(npairs);
-        if (npairs > 0) {
-            hipLaunchKernelGGL(res_pairs_kernel<false>, dim3(grid), dim3(256), 0, s, clauses.as<uint64_t>(), W, jlo,
-                               npairs, d_count, d_empty, nullptr, (int64_t)0);
-            SATMI_HIP(hipGetLastError());
+        if (!sweep(false, npairs, jlo, 0, &rc)) {
+            if (rc) return rc;
+            break;   // deadline inside the pass
         }
         SATMI_HIP(hipMemcpyAsync(&hc, counters.p, 16, hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
@@ -323,12 +406,13 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
         const int64_t ncand = (int64_t)hc.count;
         int64_t nnew = 0;
         if (ncand > 0) {
-            // the pass's working set: candidate keys + four int64 arrays of the
-            // sort/dedup; refuse (SATMI_ERR_NOMEM) rather than oversubscribe HBM
-            const double need = (double)ncand * (8.0 * K + 32.0) + 8.0 * (double)(nseen + ncand) * K;
+            // the pass's working set: candidate keys, flag / pos, the hash table and
+            // the grown clause array; refuse (SATMI_ERR_NOMEM) rather than oversubscribe HBM
+            const double need = (double)ncand * (8.0 * K + 16.0) + 8.0 * (double)HashDedup::table_slots(ncl + ncand) +
+                                8.0 * (double)(ncl + ncand) * K;
             size_t free_b = 0, total_b = 0;
             SATMI_HIP(hipMemGetInfo(&free_b, &total_b));
-            if (need > 0.8 * (double)free_b) {
+            if (need > 0.8 * (double)(free_b + cand.cap + dd.table.cap + dd.flag.cap + dd.pos.cap)) {
                 set_error("satmi_resolution_host: pass " + std::to_string(passes + 1) + " has " +
                           std::to_string(ncand) + " candidate resolvents, needing " +
                           std::to_string(need / 1e9) + " GB of device memory (" + std::to_string(free_b / 1e9) +
@@ -336,40 +420,19 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
                 return SATMI_ERR_NOMEM;
             }
             SATMI_TRY(cand.reserve(8 * (size_t)ncand * K));
-            SATMI_HIP(hipMemsetAsync(counters.p, 0, 16, s));
-            hipLaunchKernelGGL(res_pairs_kernel<true>, dim3(grid), dim3(256), 0, s, clauses.as<uint64_t>(), W, jlo,
-                               npairs, d_count, d_empty, cand.as<uint64_t>(), ncand);
-            SATMI_HIP(hipGetLastError());
-            SATMI_TRY(dd.run(cand.as<uint64_t>(), ncand, seen.as<uint64_t>(), nseen, K, newk, &nnew, s));
+            const unsigned long long start = (unsigned long long)slot_base;
+            SATMI_HIP(hipMemcpyAsync(d_count, &start, 8, hipMemcpyHostToDevice, s));
+            if (!sweep(true, npairs, jlo, ncand, &rc)) {
+                if (rc) return rc;
+                break;
+            }
+            SATMI_TRY(dd.run(clauses.as<uint64_t>(), ncl, cand.as<uint64_t>(), ncand, slot_base, K, &nnew, s));
         }
         if (nnew == 0) {   // no new clauses can be derived (REF.py:91-92)
             *h_result = 1;
             break;
         }
-        // record the pass (REF.py:94 `seen.update(new_clauses)`)
-        if (h_pass_new && passes < pass_cap) h_pass_new[passes] = nnew;
-        if (h_rec_lits && h_rec_clause_off && h_rec_pass_off && passes + 1 < rec_pass_cap) {
-            hkeys.resize((size_t)nnew * K);
-            SATMI_HIP(hipMemcpyAsync(hkeys.data(), newk.p, 8 * (size_t)nnew * K, hipMemcpyDeviceToHost, s));
-            SATMI_HIP(hipStreamSynchronize(s));
-            std::vector<int32_t> cl;
-            for (int64_t c = 0; c < nnew && rec_clauses + 1 < rec_clause_cap; ++c) {
-                cl.clear();
-                const uint64_t *k = hkeys.data() + c * K;
-                for (int d = 0; d < V; ++d) {
-                    if ((k[d >> 6] >> (d & 63)) & 1ull) cl.push_back(dense2var[d]);
-                    if ((k[W + (d >> 6)] >> (d & 63)) & 1ull) cl.push_back(-dense2var[d]);
-                }
-                std::sort(cl.begin(), cl.end());
-                if (rec_lits + (int64_t)cl.size() > rec_lit_cap) break;
-                std::copy(cl.begin(), cl.end(), h_rec_lits + rec_lits);
-                rec_lits += (int64_t)cl.size();
-                h_rec_clause_off[++rec_clauses] = rec_lits;
-            }
-            h_rec_pass_off[passes + 1] = rec_clauses;
-        }
-        ++passes;
-        // clauses.extend(new) and seen |= new
+        // clauses.extend(new) (REF.py:94-95): append the claimed candidates
         const int64_t ncl2 = ncl + nnew;
         if ((size_t)ncl2 * K * 8 > clauses.cap) {
             DevBuf grown;
@@ -377,17 +440,38 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
             SATMI_HIP(hipMemcpyAsync(grown.p, clauses.p, 8 * (size_t)ncl * K, hipMemcpyDeviceToDevice, s));
             std::swap(grown.p, clauses.p);
             std::swap(grown.cap, clauses.cap);
+            SATMI_HIP(hipStreamSynchronize(s));   // before `grown` frees the old array
         }
-        SATMI_HIP(hipMemcpyAsync(clauses.as<uint64_t>() + ncl * K, newk.p, 8 * (size_t)nnew * K,
-                                 hipMemcpyDeviceToDevice, s));
-        SATMI_TRY(seen2.reserve(8 * (size_t)(nseen + nnew) * K));
-        hipLaunchKernelGGL(res_merge_kernel, dim3(grid_for(nseen + nnew)), dim3(PRIM_BLOCK), 0, s,
-                           KeyView{seen.as<uint64_t>(), K}, nseen, KeyView{newk.as<uint64_t>(), K}, nnew,
-                           seen2.as<uint64_t>());
+        hipLaunchKernelGGL(res_append_kernel, dim3(grid_for(ncand)), dim3(PRIM_BLOCK), 0, s, cand.as<uint64_t>(),
+                           dd.flag.as<int64_t>(), dd.pos.as<int64_t>(), ncand, K, clauses.as<uint64_t>() + ncl * K);
         SATMI_HIP(hipGetLastError());
-        std::swap(seen.p, seen2.p);
-        std::swap(seen.cap, seen2.cap);
-        nseen += nnew;
+        if (h_pass_new && passes < pass_cap) h_pass_new[passes] = nnew;
+        if (h_rec_lits && h_rec_clause_off && h_rec_pass_off && passes + 1 < rec_pass_cap) {
+            // the pass's new clause set, each clause as ascending literals, the
+            // clauses in ascending order (deterministic whatever the append order)
+            hkeys.resize((size_t)nnew * K);
+            SATMI_HIP(hipMemcpyAsync(hkeys.data(), clauses.as<uint64_t>() + ncl * K, 8 * (size_t)nnew * K,
+                                     hipMemcpyDeviceToHost, s));
+            SATMI_HIP(hipStreamSynchronize(s));
+            std::vector<std::vector<int32_t>> pass(nnew);
+            for (int64_t c = 0; c < nnew; ++c) {
+                const uint64_t *k = hkeys.data() + c * K;
+                for (int d = 0; d < V; ++d) {
+                    if ((k[d >> 6] >> (d & 63)) & 1ull) pass[c].push_back(dense2var[d]);
+                    if ((k[W + (d >> 6)] >> (d & 63)) & 1ull) pass[c].push_back(-dense2var[d]);
+                }
+                std::sort(pass[c].begin(), pass[c].end());
+            }
+            std::sort(pass.begin(), pass.end());
+            for (const auto &cl : pass) {
+                if (rec_clauses + 1 >= rec_clause_cap || rec_lits + (int64_t)cl.size() > rec_lit_cap) break;
+                std::copy(cl.begin(), cl.end(), h_rec_lits + rec_lits);
+                rec_lits += (int64_t)cl.size();
+                h_rec_clause_off[++rec_clauses] = rec_lits;
+            }
+            h_rec_pass_off[passes + 1] = rec_clauses;
+        }
+        ++passes;
         jlo = ncl;
         ncl = ncl2;
         if (clause_limit > 0 && ncl > clause_limit) break;

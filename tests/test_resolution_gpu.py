@@ -68,3 +68,35 @@ def test_pigeonhole_php43_four_passes():
     r = resolve(f, max_passes=4)
     assert r["result"] == -1 and r["passes"] == 4
     assert r["pass_new"] == [36, 270, 7132, 163954]
+
+
+@pytest.mark.parametrize("base", [(1 << 31) - 37, (1 << 32) - 50])
+def test_append_slots_past_2_31(base):
+    """The pair kernel's candidate slots start at `base` (test knob): the first
+    passes of PHP(4,3) write slots across 2^31 / 2^32 (the 64-bit slot
+    broadcast and the dedup's int64 candidate indices) and must add exactly
+    the oracle's clause sets."""
+    from satmi import _capi
+    L = _capi.load()
+    f = cnf.pigeonhole(3)
+    o = oracle.resolution(f, record=True, max_passes=3)
+    _capi.check(L.satmi_resolution_debug_slot_base(base), "slot base")
+    try:
+        r = resolve(f, record=True, max_passes=3)
+    finally:
+        _capi.check(L.satmi_resolution_debug_slot_base(0), "slot base reset")
+    assert sum(r["pass_new"]) > 7000
+    assert r["result"] == o["result"] and r["pass_new"] == o["pass_new"]
+    assert [sorted(p) for p in r["clauses"]] == [sorted(p) for p in o["clauses"]]
+
+
+def test_deadline_inside_a_pass():
+    """Pass 5 of PHP(4,3) resolves 1.5e10 pairs, in launches of 2^30: the
+    deadline is checked between them, so the saturation stops as a timeout
+    (result -1 after the 4 completed passes) instead of running the pass out."""
+    import time
+    t = time.perf_counter()
+    r = resolve(cnf.pigeonhole(3), time_limit=0.5)
+    dt = time.perf_counter() - t
+    assert r["result"] == -1 and r["passes"] == 4, r
+    assert dt < 20.0, dt
