@@ -187,12 +187,37 @@ def issue_roofline(preset, per_gpu, kernel_ms):
             "clock_hz": e["effective_clock_hz"], "source": e["source"], "stale": e["kernel_src_sha256_16"] != sha}
 
 
+def saturation_roofline(workload, stats, last):
+    """Resolution (php-res): the dominant of its two kernels per step, timed by
+    HIP events on the library's stream (satmi_resolution_last_stats).  Claim
+    kernel (hash dedup): per candidate its key (8K B) read, one table slot
+    read + CAS (16 B), the occupant's key compared (8K B), flag + slot written
+    (16 B); pair kernel: per pair key i read (8K B), per candidate its key
+    written (8K B); K = 2 x 64-bit words per clause for <= 64 variables."""
+    if workload != "php-res" or not stats:
+        return None
+    K = 2   # PHP(4,3): 12 variables -> one word per sign
+    cand = sum(s["candidates"] for s in stats) / len(stats)
+    pairs = sum(s["pairs"] for s in stats) / len(stats)
+    cms = sum(s["claim_ms"] for s in stats) / len(stats)
+    pms = sum(s["pair_ms"] for s in stats) / len(stats)
+    claim_b = cand * (16 * K + 32)
+    pair_b = pairs * 8 * K + cand * 8 * K
+    name, b, ms = ("ht_cand_kernel (hash claims)", claim_b, cms) if cms >= pms else \
+        ("res_pairs_kernel", pair_b, pms)
+    ach = b / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": None, "kernel": name, "kernel_ms_per_step": ms, "algorithmic_bytes_per_step": b,
+            "candidates_per_step": cand, "pairs_per_step": pairs, "pair_ms_per_step": pms, "claim_ms_per_step": cms}
+
+
 def saturation_main(args):
     """configs[3]: Davis-Putnam / resolution saturation of a pigeonhole formula.
     A step = one full satmi_dp_host / satmi_resolution_host call (host arrays in,
     verdict out: the boundary these solvers have, REF.py:63-130).  Each rank
     solves its own replica (one formula does not shard)."""
     from satmi.dp import eliminate
+    from satmi.resolution import last_stats as res_stats
     from satmi.resolution import resolve
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -219,9 +244,12 @@ def saturation_main(args):
     t0 = time.perf_counter()
     done = 0
     last = None
+    stats = []
     for _ in range(args.steps):
         last = run()
         done += work(last)
+        if args.workload == "php-res":
+            stats.append(res_stats())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -236,9 +264,7 @@ def saturation_main(args):
            "config": {"workload": metric_desc + " (BASELINE configs[3]); replicas across ranks",
                       "preset": args.workload, "parallelism": f"replicas x{world}"},
            "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
-           # a chain of small dependent kernels per step (pair / sort / merge, or split /
-           # resolve / subsume): no single dominant kernel; rocprofv3 per-kernel stats in profiles/
-           "roofline": None}
+           "roofline": saturation_roofline(args.workload, stats, last)}
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.profile_steps:

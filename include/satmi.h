@@ -131,6 +131,11 @@ int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, const int32
                           int32_t *h_rec_lits, int64_t rec_lit_cap, int64_t *h_rec_clause_off,
                           int64_t rec_clause_cap, int64_t *h_rec_pass_off, int rec_pass_cap);
 
+/* Work of the last satmi_resolution_host call: pairs resolved, candidate
+ * resolvents generated, and the device time of its pair and claim (hash dedup)
+ * launches (HIP events on its stream), for rooflines. */
+int satmi_resolution_last_stats(int64_t *pairs, int64_t *candidates, double *pair_ms, double *claim_ms);
+
 /* Test knob: the pair kernel's first candidate append slot (default 0), so a
  * small pass exercises the slot arithmetic past 2^31 / 2^32 candidates. */
 int satmi_resolution_debug_slot_base(int64_t base);

@@ -8,18 +8,22 @@
 //
 //   * a clause is a key of K = 2W uint64 words: positive / negative literal
 //     bitsets over the formula's dense variable index (encode_keys_kernel);
-//   * pair kernel (one thread per pair, grid-stride): clash = (Pi & Nj) | (Ni & Pj).
+//   * pair kernel (a workgroup per clause j, its key in registers, 256 keys i
+//     per step): clash = (Pi & Nj) | (Ni & Pj).
 //     Two or more clashing variables make every resolvent a tautology (the
 //     other clash survives in both signs); with exactly one, the resolvent is
 //     (Pi|Pj, Ni|Nj) minus that variable, a tautology iff its two halves meet,
 //     empty iff both are zero.  Candidates are appended with one atomic per
 //     wavefront (ballot + popcount);
 //   * hash dedup: one open-addressing table per pass over every clause key
-//     (the reference's `seen`), then every candidate claims its key's slot
-//     run with a 64-bit CAS; the claimers are the pass's new clauses,
+//     (the reference's `seen`); every candidate claims its key's slot run
+//     with a 64-bit CAS, and the claimers -- the pass's new clauses -- are
 //     compacted (flag scan) and appended to the clause array;
-//   * a pass's pairs run in launches of PAIR_CHUNK, the deadline checked
-//     between them, so a long pass ends as a timeout (REF.py:417-437);
+//   * a pass runs in chunks of about PAIR_CHUNK pairs: candidates of a chunk
+//     (a buffer of the chunk's worst case), their claims, the winners
+//     appended -- memory is bounded by the chunk and the new clauses, not by
+//     the pass's candidates -- and the deadline is checked between chunks, so
+//     a long pass ends as a timeout (REF.py:417-437);
 //   * semi-naive passes: pairs whose newer clause was added in the previous pass
 //     (all pairs in pass 1) -- every older pair was resolved in an earlier pass
 //     and its resolvents are already in `seen`, so the new set is identical.
@@ -53,83 +57,117 @@ __global__ void encode_keys_kernel(int nclauses, const int32_t *off, const int32
 
 __device__ __forceinline__ int64_t tri(int64_t j) { return j * (j - 1) / 2; }   // pairs (i<j') with j' < j
 
-// Pairs (i < j) with j in [jlo, N).  WRITE=false: count candidates; WRITE=true:
-// append them to cand (slots from *count, which must start at 0).
-// Pairs are numbered q = tri(j) + i over the whole pass; this launch takes
-// q in [tri(jlo) + p_begin, tri(jlo) + p_begin + npairs) (a chunk of the pass).
-// WRITE: candidate slot k (from *count, which starts at `slot_base`) goes to
-// cand[k - slot_base].
-template <bool WRITE>
-__global__ void __launch_bounds__(256) res_pairs_kernel(const uint64_t *keys, int W, int64_t jlo, int64_t p_begin,
-                                                        int64_t npairs, unsigned long long *count, int *empty_found,
+// The resolvent of keys a and b on their single clashing variable
+// (word cw, bit cbit): (Pa|Pb, Na|Nb) minus that variable.
+template <typename KB>
+__device__ __forceinline__ void resolvent(const uint64_t *a, KB &&B, int W, int cw, uint64_t cbit, uint64_t *r) {
+    for (int w = 0; w < W; ++w) {
+        uint64_t rp = a[w] | B(w), rn = a[W + w] | B(W + w);
+        if (w == cw) {
+            rp &= ~cbit;
+            rn &= ~cbit;
+        }
+        r[w] = rp;
+        r[W + w] = rn;
+    }
+}
+
+// Classify pair (a, b): 1 = candidate resolvent (clash word / bit out), 0 =
+// no resolvent or a tautology, 2 = the empty resolvent.
+template <int WT, typename KB>
+__device__ __forceinline__ int classify(const uint64_t *a, KB &&B, int W, int *cw, uint64_t *cbit) {
+    int nclash = 0;
+#pragma unroll
+    for (int w0 = 0; w0 < (WT ? WT : 1); ++w0) {
+        for (int w = w0; w < W; w += (WT ? WT : 1)) {
+            const uint64_t c = (a[w] & B(W + w)) | (a[W + w] & B(w));
+            if (c) {
+                nclash += __popcll(c);
+                *cw = w;
+                *cbit = c & (~c + 1ull);
+            }
+        }
+    }
+    if (nclash != 1) return 0;   // no clash, or >= 2: every resolvent is a tautology
+    bool taut = false, empty = true;
+    for (int w = 0; w < W; ++w) {
+        uint64_t rp = a[w] | B(w), rn = a[W + w] | B(W + w);
+        if (w == *cw) {
+            rp &= ~*cbit;
+            rn &= ~*cbit;
+        }
+        taut |= (rp & rn) != 0ull;
+        empty &= (rp | rn) == 0ull;
+    }
+    return taut ? 0 : (empty ? 2 : 1);
+}
+
+// Pairs (i, j), i < j, for j in [j_begin, j_end): one workgroup per clause j
+// (grid-stride), 256 i's per step -- key j stays in registers (WT = W words
+// per sign known at compile time; WT = 0 reads it from memory), keys i stream
+// coalesced.  The candidates' i indices collect in an LDS buffer and are
+// flushed with ONE append atomic per buffer (a single global counter takes
+// under ~90 atomics per microsecond chip-wide: one per wavefront step was the
+// kernel's bound); slot k (from *count, started at `slot_base`) goes to
+// cand[k - slot_base] when it fits in cand_cap -- a sweep that overflows is
+// re-run with a larger buffer.
+constexpr int PAIR_BUF = 2048;
+template <int WT>
+__global__ void __launch_bounds__(256) res_pairs_kernel(const uint64_t *keys, int Wrt, int64_t j_begin, int64_t j_end,
+                                                        unsigned long long *count, int *empty_found,
                                                         uint64_t *cand, int64_t cand_cap, int64_t slot_base) {
+    __shared__ int32_t ibuf[PAIR_BUF];
+    __shared__ int nbuf;
+    __shared__ unsigned long long base_sh;
+    const int W = WT ? WT : Wrt;
     const int K = 2 * W;
     const int ln = lane_id();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t base = tri(jlo) + p_begin;
-    for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x; p0 < npairs; p0 += stride) {
-        const int64_t p = p0 + threadIdx.x;
-        bool is_cand = false;
-        int cw = 0;
-        uint64_t cbit = 0;
-        int64_t i = 0, j = 0;
-        if (p < npairs) {
-            const int64_t q = p + base;
-            j = (int64_t)((1.0 + sqrt(1.0 + 8.0 * (double)q)) * 0.5);
-            while (tri(j) > q) --j;
-            while (tri(j + 1) <= q) ++j;
-            i = q - tri(j);
-            const uint64_t *a = keys + i * K, *b = keys + j * K;
-            int nclash = 0;
-            for (int w = 0; w < W; ++w) {
-                const uint64_t c = (a[w] & b[W + w]) | (a[W + w] & b[w]);
-                if (c) {
-                    nclash += __popcll(c);
-                    cw = w;
-                    cbit = c & (~c + 1ull);
-                }
-            }
-            if (nclash == 1) {
-                bool taut = false, empty = true;
-                for (int w = 0; w < W; ++w) {
-                    uint64_t rp = a[w] | b[w], rn = a[W + w] | b[W + w];
-                    if (w == cw) {
-                        rp &= ~cbit;
-                        rn &= ~cbit;
-                    }
-                    taut |= (rp & rn) != 0ull;
-                    empty &= (rp | rn) == 0ull;
-                }
-                if (!taut) {
-                    if (empty) *empty_found = 1;   // REF.py:84-85
-                    else is_cand = true;
-                }
-            }
+    if (threadIdx.x == 0) nbuf = 0;
+    __syncthreads();
+    for (int64_t j = j_begin + blockIdx.x; j < j_end; j += gridDim.x) {
+        const uint64_t *b = keys + j * K;
+        uint64_t bj[WT ? 2 * WT : 1];
+        if constexpr (WT > 0) {
+#pragma unroll
+            for (int w = 0; w < 2 * WT; ++w) bj[w] = b[w];
         }
-        const uint64_t m = __ballot(is_cand);
-        if (m == 0ull) continue;
-        unsigned long long slot0 = 0;
-        if (ln == 0) slot0 = atomicAdd(count, (unsigned long long)__popcll(m));
-        // zero-extend each 32-bit half (a sign-extended low half past 2^31
-        // candidates would turn the slot negative and the write out of bounds)
-        slot0 = (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)slot0) |
-                ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(slot0 >> 32)) << 32);
-        if (WRITE && is_cand) {
-            const int64_t slot = (int64_t)slot0 + __popcll(m & lanemask_lt()) - slot_base;
-            if (slot >= 0 && slot < cand_cap) {
-                const uint64_t *a = keys + i * K, *b = keys + j * K;
-                uint64_t *r = cand + slot * K;
-                for (int w = 0; w < W; ++w) {
-                    uint64_t rp = a[w] | b[w], rn = a[W + w] | b[W + w];
-                    if (w == cw) {
-                        rp &= ~cbit;
-                        rn &= ~cbit;
-                    }
-                    r[w] = rp;
-                    r[W + w] = rn;
-                }
+        const auto B = [&](int w) { return WT ? bj[WT ? w : 0] : b[w]; };
+        const auto flush = [&]() {
+            // block-uniform: called between __syncthreads with nbuf settled
+            const int n = nbuf;
+            if (threadIdx.x == 0) base_sh = atomicAdd(count, (unsigned long long)n);
+            __syncthreads();
+            const int64_t base = (int64_t)base_sh - slot_base;
+            for (int t = threadIdx.x; t < n; t += blockDim.x) {
+                const int64_t slot = base + t;
+                if (slot < 0 || slot >= cand_cap) continue;
+                const uint64_t *a = keys + (int64_t)ibuf[t] * K;
+                int cw = 0;
+                uint64_t cbit = 0;
+                (void)classify<WT>(a, B, W, &cw, &cbit);
+                resolvent(a, B, W, cw, cbit, cand + slot * K);
             }
+            __syncthreads();
+            if (threadIdx.x == 0) nbuf = 0;
+            __syncthreads();
+        };
+        for (int64_t i0 = 0; i0 < j; i0 += blockDim.x) {
+            const int64_t i = i0 + threadIdx.x;
+            int cls = 0, cw = 0;
+            uint64_t cbit = 0;
+            if (i < j) cls = classify<WT>(keys + i * K, B, W, &cw, &cbit);
+            if (cls == 2) *empty_found = 1;   // REF.py:84-85
+            const uint64_t m = __ballot(cls == 1);
+            if (m) {
+                int pos = 0;
+                if (ln == 0) pos = atomicAdd(&nbuf, __popcll(m));
+                pos = uniform_i32(pos) + __popcll(m & lanemask_lt());
+                if (cls == 1) ibuf[pos] = (int32_t)i;
+            }
+            __syncthreads();
+            if (nbuf > PAIR_BUF - (int)blockDim.x) flush();
         }
+        if (nbuf > 0) flush();
     }
 }
 
@@ -170,37 +208,45 @@ __device__ __forceinline__ bool key_eq(const uint64_t *a, const uint64_t *b, int
     return true;
 }
 
-// Claim a slot for value v (key x).  Returns true with *slot if x was absent.
-__device__ bool ht_insert(uint64_t *table, uint64_t mask, const KeySrc &S, uint64_t v, const uint64_t *x) {
+// Claim a slot for value v (key x): the slot if x was absent, else -1.
+__device__ int64_t ht_insert(uint64_t *table, uint64_t mask, const KeySrc &S, uint64_t v, const uint64_t *x) {
     uint64_t s = key_hash(x, S.K) & mask;
     for (;;) {
         uint64_t cur = __hip_atomic_load(table + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur == HT_EMPTY) {
             cur = atomicCAS((unsigned long long *)(table + s), (unsigned long long)HT_EMPTY, (unsigned long long)v);
-            if (cur == HT_EMPTY) return true;
+            if (cur == HT_EMPTY) return (int64_t)s;
         }
-        if (key_eq(S.at(cur), x, S.K)) return false;
+        if (key_eq(S.at(cur), x, S.K)) return -1;
         s = (s + 1) & mask;
     }
 }
 
-__global__ void ht_clauses_kernel(uint64_t *table, uint64_t mask, KeySrc S, int64_t ncl) {
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncl; c += (int64_t)gridDim.x * blockDim.x)
+// clauses [c0, c1) into the table (an input clause equal to an earlier one stays out)
+__global__ void ht_clauses_kernel(uint64_t *table, uint64_t mask, KeySrc S, int64_t c0, int64_t c1) {
+    for (int64_t c = c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < c1; c += (int64_t)gridDim.x * blockDim.x)
         (void)ht_insert(table, mask, S, (uint64_t)c, S.clauses + c * S.K);
 }
 
-// flag[t] = candidate t claimed its key (new in this pass)
-__global__ void ht_cand_kernel(uint64_t *table, uint64_t mask, KeySrc S, int64_t n, int64_t *flag) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
-        flag[t] = ht_insert(table, mask, S, CAND_BIT | (uint64_t)(S.base + t), S.cand + t * S.K) ? 1 : 0;
+// flag[t] = candidate t claimed its key (new in this pass), slot[t] its table slot
+__global__ void ht_cand_kernel(uint64_t *table, uint64_t mask, KeySrc S, int64_t n, int64_t *flag, int64_t *slot) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t sl = ht_insert(table, mask, S, CAND_BIT | (uint64_t)(S.base + t), S.cand + t * S.K);
+        flag[t] = sl >= 0 ? 1 : 0;
+        slot[t] = sl;
+    }
 }
 
-// clauses.extend(new): the claimed candidates, in append order, after clause ncl
-__global__ void res_append_kernel(const uint64_t *cand, const int64_t *flag, const int64_t *pos, int64_t n, int K,
-                                  uint64_t *dst) {
+// clauses.extend(new): the claimed candidates become clauses first .. first +
+// count, in append order; their table entries are re-pointed at the clause
+// array (the candidate buffer is reused by the next chunk)
+__global__ void res_append_kernel(const uint64_t *cand, const int64_t *flag, const int64_t *pos, const int64_t *slot,
+                                  int64_t n, int K, uint64_t *clauses, int64_t first, uint64_t *table) {
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
         if (!flag[t]) continue;
-        for (int w = 0; w < K; ++w) dst[pos[t] * K + w] = cand[t * K + w];
+        const int64_t c = first + pos[t];
+        for (int w = 0; w < K; ++w) clauses[c * K + w] = cand[t * K + w];
+        __hip_atomic_store(table + slot[t], (uint64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -233,53 +279,70 @@ struct DevBuf {
         if (_rc != SATMI_OK) return _rc; \
     } while (0)
 
-// One pass's dedup (see ht_insert): a fresh table over every clause key, then
-// the candidates' claims; flag / pos (exclusive scan) give the new keys in
-// append order, *nnew their count.
-struct HashDedup {
-    DevBuf table, flag, pos, tiles, grand;
-    static uint64_t table_slots(int64_t keys) {
-        uint64_t cap = 64;
-        while (cap < 2 * (uint64_t)keys) cap <<= 1;
-        return cap;
-    }
-    int run(const uint64_t *clauses, int64_t ncl, const uint64_t *cand, int64_t n, int64_t slot_base, int K,
-            int64_t *nnew, hipStream_t s) {
-        *nnew = 0;
-        if (n == 0) return SATMI_OK;
-        const uint64_t cap = table_slots(ncl + n);
-        SATMI_TRY(table.reserve(8 * cap));
-        SATMI_TRY(flag.reserve(8 * (size_t)n));
-        SATMI_TRY(pos.reserve(8 * (size_t)n));
-        SATMI_TRY(tiles.reserve(8 * (size_t)((n + SCAN_TILE - 1) / SCAN_TILE + 1)));
-        SATMI_TRY(grand.reserve(8));
-        SATMI_HIP(hipMemsetAsync(table.p, 0xFF, 8 * cap, s));   // HT_EMPTY
-        const KeySrc S{clauses, cand, slot_base, K};
-        if (ncl > 0)
-            hipLaunchKernelGGL(ht_clauses_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(),
-                               cap - 1, S, ncl);
-        hipLaunchKernelGGL(ht_cand_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(), cap - 1,
-                           S, n, flag.as<int64_t>());
-        SATMI_HIP(hipGetLastError());
-        SATMI_TRY(exclusive_scan(flag.as<int64_t>(), pos.as<int64_t>(), n, tiles.as<int64_t>(),
-                                 grand.as<int64_t>(), s));
-        SATMI_HIP(hipMemcpyAsync(nnew, grand.p, 8, hipMemcpyDeviceToHost, s));
-        SATMI_HIP(hipStreamSynchronize(s));
-        return SATMI_OK;
-    }
-};
+uint64_t table_slots(int64_t keys) {
+    uint64_t cap = 1024;
+    while (cap < 2 * (uint64_t)keys) cap <<= 1;
+    return cap;
+}
 
-// pairs per launch: a pass is cut into launches of this many pairs so that the
-// deadline is checked inside a long pass (REF.py:417-437's timeout)
-constexpr int64_t PAIR_CHUNK = 1ll << 30;
+// Pairs per chunk of a pass: the candidate buffer holds one chunk's worst
+// case (every pair a candidate), so a chunk never overflows; the deadline is
+// checked between chunks, so a long pass ends as a timeout (REF.py:417-437).
+constexpr int64_t PAIR_CHUNK = 1ll << 27;
 
 int64_t g_slot_base = 0;   // test knob: first append slot of the pair kernel
+
+// Work and kernel time of the last satmi_resolution_host call (HIP events on
+// its stream around the pair and claim launches): bench.py's roofline input.
+struct ResStats {
+    int64_t pairs = 0, candidates = 0, keys_tabled = 0;
+    double pair_ms = 0.0, claim_ms = 0.0;
+};
+ResStats g_stats;
+
+// Times launches on one stream: begin() / end() bracket them, total() sums.
+struct EventTimer {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    size_t used = 0;
+    ~EventTimer() {
+        for (auto &e : ev) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+    }
+    hipEvent_t begin(hipStream_t s) {
+        if (used == ev.size()) {
+            hipEvent_t a = nullptr, b = nullptr;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return nullptr;
+            ev.push_back({a, b});
+        }
+        (void)hipEventRecord(ev[used].first, s);
+        return ev[used].first;
+    }
+    void end(hipStream_t s) { (void)hipEventRecord(ev[used++].second, s); }
+    double total() {   // after the stream drained
+        double ms = 0.0;
+        for (size_t i = 0; i < used; ++i) {
+            float t = 0.0f;
+            if (hipEventElapsedTime(&t, ev[i].first, ev[i].second) == hipSuccess) ms += t;
+        }
+        return ms;
+    }
+};
 
 }  // namespace
 
 }  // namespace satmi
 
 using namespace satmi;
+
+extern "C" int satmi_resolution_last_stats(int64_t *pairs, int64_t *candidates, double *pair_ms, double *claim_ms) {
+    if (pairs) *pairs = g_stats.pairs;
+    if (candidates) *candidates = g_stats.candidates;
+    if (pair_ms) *pair_ms = g_stats.pair_ms;
+    if (claim_ms) *claim_ms = g_stats.claim_ms;
+    return SATMI_OK;
+}
 
 extern "C" int satmi_resolution_debug_slot_base(int64_t base) {
     if (base < 0 || base > (1ll << 61)) {
@@ -347,104 +410,137 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
                            clauses.as<uint64_t>());
         SATMI_HIP(hipGetLastError());
     }
-    HashDedup dd;
+    DevBuf table, flag, pos, slotv, tiles, grand;
+    EventTimer t_pairs, t_claims;
+    g_stats = ResStats{};
+    uint64_t tcap = 0;
     unsigned long long *d_count = counters.as<unsigned long long>();
     int *d_empty = (int *)(counters.as<char>() + 8);
-    // one sweep of the pass's pairs (count or write), a launch per PAIR_CHUNK;
-    // false if the deadline passed between two launches
-    const auto sweep = [&](bool write, int64_t npairs, int64_t jlo, int64_t ncand, int *rc) {
-        *rc = SATMI_OK;
-        for (int64_t p = 0; p < npairs; p += PAIR_CHUNK) {
-            if (p > 0) {
-                if (hipStreamSynchronize(s) != hipSuccess) {
-                    *rc = hip_fail(hipGetLastError(), "resolution pair sweep");
-                    return false;
-                }
-                if (expired()) return false;
-            }
-            const int64_t np = std::min(PAIR_CHUNK, npairs - p);
-            if (write)
-                hipLaunchKernelGGL(res_pairs_kernel<true>, dim3(grid_for(np)), dim3(256), 0, s,
-                                   clauses.as<uint64_t>(), W, jlo, p, np, d_count, d_empty, cand.as<uint64_t>(),
-                                   ncand, slot_base);
-            else
-                hipLaunchKernelGGL(res_pairs_kernel<false>, dim3(grid_for(np)), dim3(256), 0, s,
-                                   clauses.as<uint64_t>(), W, jlo, p, np, d_count, d_empty, nullptr, (int64_t)0,
-                                   (int64_t)0);
-            if (hipGetLastError() != hipSuccess) {
-                *rc = hip_fail(hipErrorLaunchFailure, "res_pairs_kernel");
-                return false;
-            }
+    // a fresh table holding clauses [0, nkeys) with room for `room` keys
+    const auto rebuild_table = [&](int64_t nkeys, int64_t room) {
+        tcap = table_slots(room);
+        SATMI_TRY(table.reserve(8 * tcap));
+        SATMI_HIP(hipMemsetAsync(table.p, 0xFF, 8 * tcap, s));   // HT_EMPTY
+        if (nkeys > 0)
+            hipLaunchKernelGGL(ht_clauses_kernel, dim3(grid_for(nkeys)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(),
+                               tcap - 1, KeySrc{clauses.as<uint64_t>(), nullptr, 0, K}, (int64_t)0, nkeys);
+        SATMI_HIP(hipGetLastError());
+        return SATMI_OK;
+    };
+    const auto launch_pairs = [&](int64_t j0, int64_t j1, int64_t cap) {
+        const int grid = (int)std::min<int64_t>(j1 - j0, 65536);
+        switch (W) {
+            case 1:
+                hipLaunchKernelGGL(res_pairs_kernel<1>, dim3(grid), dim3(256), 0, s, clauses.as<uint64_t>(), W, j0, j1,
+                                   d_count, d_empty, cand.as<uint64_t>(), cap, slot_base);
+                break;
+            case 2:
+                hipLaunchKernelGGL(res_pairs_kernel<2>, dim3(grid), dim3(256), 0, s, clauses.as<uint64_t>(), W, j0, j1,
+                                   d_count, d_empty, cand.as<uint64_t>(), cap, slot_base);
+                break;
+            case 3:
+                hipLaunchKernelGGL(res_pairs_kernel<3>, dim3(grid), dim3(256), 0, s, clauses.as<uint64_t>(), W, j0, j1,
+                                   d_count, d_empty, cand.as<uint64_t>(), cap, slot_base);
+                break;
+            case 4:
+                hipLaunchKernelGGL(res_pairs_kernel<4>, dim3(grid), dim3(256), 0, s, clauses.as<uint64_t>(), W, j0, j1,
+                                   d_count, d_empty, cand.as<uint64_t>(), cap, slot_base);
+                break;
+            default:
+                hipLaunchKernelGGL(res_pairs_kernel<0>, dim3(grid), dim3(256), 0, s, clauses.as<uint64_t>(), W, j0, j1,
+                                   d_count, d_empty, cand.as<uint64_t>(), cap, slot_base);
         }
-        return true;
+    };
+    const auto grow_clauses = [&](int64_t want) {
+        if ((size_t)want * K * 8 <= clauses.cap) return SATMI_OK;
+        DevBuf grown;
+        SATMI_TRY(grown.reserve(8 * (size_t)want * K * 2));
+        SATMI_HIP(hipMemcpyAsync(grown.p, clauses.p, clauses.cap, hipMemcpyDeviceToDevice, s));
+        std::swap(grown.p, clauses.p);
+        std::swap(grown.cap, clauses.cap);
+        SATMI_HIP(hipStreamSynchronize(s));   // before `grown` frees the old array
+        return SATMI_OK;
     };
 
     int64_t jlo = 0, rec_clauses = 0, rec_lits = 0;
     int passes = 0;
+    bool stopped = false;   // a limit (deadline) ended a pass early
     std::vector<uint64_t> hkeys;
-    for (;;) {
+    while (!stopped) {
         if (max_passes > 0 && passes >= max_passes) break;
         if (expired()) break;
-        const int64_t npairs = (ncl * (ncl - 1) - jlo * (jlo - 1)) / 2;
-        struct {
-            unsigned long long count;
-            int empty;
-            int pad;
-        } hc{0, 0, 0};
-        int rc = SATMI_OK;
-        SATMI_HIP(hipMemsetAsync(counters.p, 0, 16, s));
-        if (!sweep(false, npairs, jlo, 0, &rc)) {
-            if (rc) return rc;
-            break;   // deadline inside the pass
+        // one pass: chunks of pairs (i < j, j in [jlo, ncl)) -> candidates ->
+        // claims in the pass's table -> the winners appended after clause ncl
+        int64_t nnew = 0;
+        SATMI_TRY(rebuild_table(ncl, 2 * ncl + 65536));
+        bool empty = false;
+        for (int64_t j0 = jlo; j0 < ncl && !empty;) {
+            if (j0 > jlo && expired()) {
+                stopped = true;
+                break;
+            }
+            // j1: about PAIR_CHUNK pairs past j0 (tri(j1) - tri(j0)), at least one j
+            const double t1 = 0.5 * (double)j0 * (double)(j0 - 1) + (double)PAIR_CHUNK;
+            int64_t j1 = (int64_t)(0.5 + std::sqrt(0.25 + 2.0 * t1));
+            j1 = std::min(ncl, std::max(j1, j0 + 1));
+            while (j1 > j0 + 1 && (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2 > PAIR_CHUNK) --j1;
+            const int64_t cap = std::max<int64_t>(1, (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2);
+            SATMI_TRY(cand.reserve(8 * (size_t)cap * K));
+            struct {
+                unsigned long long count;
+                int empty;
+                int pad;
+            } hc{(unsigned long long)slot_base, 0, 0};
+            SATMI_HIP(hipMemcpyAsync(counters.p, &hc, 16, hipMemcpyHostToDevice, s));
+            t_pairs.begin(s);
+            launch_pairs(j0, j1, cap);
+            t_pairs.end(s);
+            g_stats.pairs += (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2;
+            SATMI_HIP(hipGetLastError());
+            SATMI_HIP(hipMemcpyAsync(&hc, counters.p, 16, hipMemcpyDeviceToHost, s));
+            SATMI_HIP(hipStreamSynchronize(s));
+            j0 = j1;
+            if (hc.empty) {   // an empty resolvent: unsatisfiable (REF.py:84-85)
+                empty = true;
+                break;
+            }
+            const int64_t nc = (int64_t)(hc.count - (unsigned long long)slot_base);
+            if (nc <= 0) continue;
+            if ((uint64_t)(ncl + nnew + nc) > tcap / 2) SATMI_TRY(rebuild_table(ncl + nnew, 2 * (ncl + nnew + nc)));
+            SATMI_TRY(flag.reserve(8 * (size_t)nc));
+            SATMI_TRY(pos.reserve(8 * (size_t)nc));
+            SATMI_TRY(slotv.reserve(8 * (size_t)nc));
+            SATMI_TRY(tiles.reserve(8 * (size_t)((nc + SCAN_TILE - 1) / SCAN_TILE + 1)));
+            SATMI_TRY(grand.reserve(8));
+            t_claims.begin(s);
+            hipLaunchKernelGGL(ht_cand_kernel, dim3(grid_for(nc)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(),
+                               tcap - 1, KeySrc{clauses.as<uint64_t>(), cand.as<uint64_t>(), slot_base, K}, nc,
+                               flag.as<int64_t>(), slotv.as<int64_t>());
+            t_claims.end(s);
+            g_stats.candidates += nc;
+            SATMI_HIP(hipGetLastError());
+            SATMI_TRY(exclusive_scan(flag.as<int64_t>(), pos.as<int64_t>(), nc, tiles.as<int64_t>(),
+                                     grand.as<int64_t>(), s));
+            int64_t nwin = 0;
+            SATMI_HIP(hipMemcpyAsync(&nwin, grand.p, 8, hipMemcpyDeviceToHost, s));
+            SATMI_HIP(hipStreamSynchronize(s));
+            if (nwin == 0) continue;
+            SATMI_TRY(grow_clauses(ncl + nnew + nwin));
+            hipLaunchKernelGGL(res_append_kernel, dim3(grid_for(nc)), dim3(PRIM_BLOCK), 0, s, cand.as<uint64_t>(),
+                               flag.as<int64_t>(), pos.as<int64_t>(), slotv.as<int64_t>(), nc, K,
+                               clauses.as<uint64_t>(), ncl + nnew, table.as<uint64_t>());
+            SATMI_HIP(hipGetLastError());
+            nnew += nwin;
         }
-        SATMI_HIP(hipMemcpyAsync(&hc, counters.p, 16, hipMemcpyDeviceToHost, s));
-        SATMI_HIP(hipStreamSynchronize(s));
-        if (hc.empty) {   // an empty resolvent: unsatisfiable (REF.py:84-85)
+        if (empty) {
             *h_result = 0;
             break;
         }
-        const int64_t ncand = (int64_t)hc.count;
-        int64_t nnew = 0;
-        if (ncand > 0) {
-            // the pass's working set: candidate keys, flag / pos, the hash table and
-            // the grown clause array; refuse (SATMI_ERR_NOMEM) rather than oversubscribe HBM
-            const double need = (double)ncand * (8.0 * K + 16.0) + 8.0 * (double)HashDedup::table_slots(ncl + ncand) +
-                                8.0 * (double)(ncl + ncand) * K;
-            size_t free_b = 0, total_b = 0;
-            SATMI_HIP(hipMemGetInfo(&free_b, &total_b));
-            if (need > 0.8 * (double)(free_b + cand.cap + dd.table.cap + dd.flag.cap + dd.pos.cap)) {
-                set_error("satmi_resolution_host: pass " + std::to_string(passes + 1) + " has " +
-                          std::to_string(ncand) + " candidate resolvents, needing " +
-                          std::to_string(need / 1e9) + " GB of device memory (" + std::to_string(free_b / 1e9) +
-                          " GB free); set clause_limit / max_passes");
-                return SATMI_ERR_NOMEM;
-            }
-            SATMI_TRY(cand.reserve(8 * (size_t)ncand * K));
-            const unsigned long long start = (unsigned long long)slot_base;
-            SATMI_HIP(hipMemcpyAsync(d_count, &start, 8, hipMemcpyHostToDevice, s));
-            if (!sweep(true, npairs, jlo, ncand, &rc)) {
-                if (rc) return rc;
-                break;
-            }
-            SATMI_TRY(dd.run(clauses.as<uint64_t>(), ncl, cand.as<uint64_t>(), ncand, slot_base, K, &nnew, s));
-        }
+        if (stopped) break;
         if (nnew == 0) {   // no new clauses can be derived (REF.py:91-92)
             *h_result = 1;
             break;
         }
-        // clauses.extend(new) (REF.py:94-95): append the claimed candidates
-        const int64_t ncl2 = ncl + nnew;
-        if ((size_t)ncl2 * K * 8 > clauses.cap) {
-            DevBuf grown;
-            SATMI_TRY(grown.reserve(8 * (size_t)ncl2 * K * 2));
-            SATMI_HIP(hipMemcpyAsync(grown.p, clauses.p, 8 * (size_t)ncl * K, hipMemcpyDeviceToDevice, s));
-            std::swap(grown.p, clauses.p);
-            std::swap(grown.cap, clauses.cap);
-            SATMI_HIP(hipStreamSynchronize(s));   // before `grown` frees the old array
-        }
-        hipLaunchKernelGGL(res_append_kernel, dim3(grid_for(ncand)), dim3(PRIM_BLOCK), 0, s, cand.as<uint64_t>(),
-                           dd.flag.as<int64_t>(), dd.pos.as<int64_t>(), ncand, K, clauses.as<uint64_t>() + ncl * K);
-        SATMI_HIP(hipGetLastError());
         if (h_pass_new && passes < pass_cap) h_pass_new[passes] = nnew;
         if (h_rec_lits && h_rec_clause_off && h_rec_pass_off && passes + 1 < rec_pass_cap) {
             // the pass's new clause set, each clause as ascending literals, the
@@ -473,10 +569,12 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
         }
         ++passes;
         jlo = ncl;
-        ncl = ncl2;
+        ncl += nnew;
         if (clause_limit > 0 && ncl > clause_limit) break;
     }
     SATMI_HIP(hipStreamSynchronize(s));
     *h_passes = passes;
+    g_stats.pair_ms = t_pairs.total();
+    g_stats.claim_ms = t_claims.total();
     return SATMI_OK;
 }

@@ -91,12 +91,14 @@ def test_append_slots_past_2_31(base):
 
 
 def test_deadline_inside_a_pass():
-    """Pass 5 of PHP(4,3) resolves 1.5e10 pairs, in launches of 2^30: the
-    deadline is checked between them, so the saturation stops as a timeout
-    (result -1 after the 4 completed passes) instead of running the pass out."""
+    """PHP(4,3) saturates through passes of 1.5e10 pairs and more (pass 6 and
+    on), run in chunks of 2^27 pairs with the deadline checked between them:
+    the saturation stops as a timeout (result -1) within a chunk of the
+    limit, after at least the passes the oracle-checked test above covers."""
     import time
     t = time.perf_counter()
     r = resolve(cnf.pigeonhole(3), time_limit=0.5)
     dt = time.perf_counter() - t
-    assert r["result"] == -1 and r["passes"] == 4, r
-    assert dt < 20.0, dt
+    assert r["result"] == -1 and r["passes"] >= 4, r
+    assert r["pass_new"][:4] == [36, 270, 7132, 163954]
+    assert dt < 10.0, dt
