@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--profile-steps", action="store_true", help="no warmup/cpu leg (for rocprofv3 runs)")
     p.add_argument("--kernel", choices=("auto", "inc", "scan", "general"), default="auto",
                    help="DPLL kernel policy (satmi_dpll_set_kernel); auto = incremental clause kernel")
+    p.add_argument("--no-split", action="store_true", help="disable branch splitting (satmi_dpll_set_split)")
+    p.add_argument("--streams", type=int, default=2, choices=(1, 2, 3, 4),
+                   help="HIP streams (each with its own resident batch) the steps rotate over")
     a = p.parse_args()
     if a.workload in SATURATION:
         return a
@@ -299,21 +302,23 @@ def main():
     L = _capi.load()
     _capi.set_kernel({"auto": _capi.KERNEL_AUTO, "inc": _capi.KERNEL_INC, "scan": _capi.KERNEL_SCAN,
                       "general": _capi.KERNEL_GENERAL}[args.kernel])
+    _capi.set_split(not args.no_split)
+    NS = args.streams
 
     n, k = args.n, args.k
     b0, b1 = shard_range(args.total, world, rank)   # this rank's contiguous shard of the step's batch
     B = b1 - b0
     m = int(round(args.alpha * n))
-    # two distinct resident batches per rank, alternated step to step
-    batches = [cnf.uniform_ksat_device(B, n, m, k, seed=args.seed + 1000 * rank + j, device=dev) for j in range(2)]
-    # Two streams, each with its own batch and output buffers: step j runs on
-    # stream j % 2, so the next batch's waves take the CU slots that the
+    # NS distinct resident batches per rank, rotated step to step
+    batches = [cnf.uniform_ksat_device(B, n, m, k, seed=args.seed + 1000 * rank + j, device=dev) for j in range(NS)]
+    # NS streams, each with its own batch and output buffers: step j runs on
+    # stream j % NS, so the next batch's waves take the CU slots that the
     # current batch's tail (its longest searches) leaves idle.  Launches on one
     # stream stay ordered, so a stream's buffers are reused only after its
     # previous step (kernel + verdict reduction) has finished.
-    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]   # non-blocking pool streams
+    streams = [torch.cuda.Stream(dev) for _ in range(NS)]   # non-blocking pool streams
     outs = []
-    for _ in range(2):
+    for _ in range(NS):
         outs.append((torch.zeros(B, dtype=torch.int32, device=dev),
                      torch.zeros((B, _capi.NCOUNTERS), dtype=torch.int64, device=dev),
                      torch.zeros(B, dtype=torch.int32, device=dev),
@@ -324,9 +329,9 @@ def main():
     spans = torch.zeros((max(args.steps, 1), 2), dtype=torch.int64, device=dev)
 
     def step(j, evs=None):
-        s = streams[j % 2]
-        icb, clb, lits, nv = batches[j % 2]
-        status, counters, sol_len, sol_lits = outs[j % 2]
+        s = streams[j % NS]
+        icb, clb, lits, nv = batches[j % NS]
+        status, counters, sol_len, sol_lits = outs[j % NS]
         with torch.cuda.stream(s):
             if evs is not None:
                 evs[0].record(s)
@@ -382,18 +387,18 @@ def main():
     kms = [a.elapsed_time(b) for a, b in evs]
     event_ms = sum(kms) / len(kms)
     totals = torch.stack(aggs).sum(dim=0)
-    status, counters, sol_len, sol_lits = outs[(args.steps - 1) % 2]
+    status, counters, sol_len, sol_lits = outs[(args.steps - 1) % NS]
     tot = totals.tolist()
     nsat, props, nodes, bad, written, ticks, all_inst = tot
     capped = args.node_limit > 0
     # node-capped workloads (configs[4]) measure search throughput: unit-props/s
     value = props / elapsed if capped else all_inst / elapsed
 
-    # correctness check outside the timed region, on BOTH resident batches (the
+    # correctness check outside the timed region, on EVERY resident batch (the
     # last step of each stream): every reported model satisfies its formula
     def models_ok_for(j):
-        icb_, clb_, lits_, nv_ = batches[j % 2]
-        status_, counters_, sol_len_, sol_lits_ = outs[j % 2]
+        icb_, clb_, lits_, nv_ = batches[j % NS]
+        status_, counters_, sol_len_, sol_lits_ = outs[j % NS]
         sat_rows = counters_[:, 5] > 0
         val = torch.zeros((B, n + 1), dtype=torch.int8, device=dev)
         live = torch.arange(n, device=dev)[None, :] < sol_len_[:, None]
@@ -405,10 +410,10 @@ def main():
         clause_ok = (litval > 0).any(dim=2).all(dim=1)
         return bool(((~sat_rows) | clause_ok).all().item())
 
-    models_ok = all(models_ok_for(j) for j in range(max(0, args.steps - 2), args.steps))
+    models_ok = all(models_ok_for(j) for j in range(max(0, args.steps - NS), args.steps))
     if not models_ok or bad:
         raise SystemExit(f"bench: invalid result (models_ok={models_ok}, limited={bad})")
-    icb, clb, lits, nv = batches[(args.steps - 1) % 2]
+    icb, clb, lits, nv = batches[(args.steps - 1) % NS]
 
     # roofline of the dominant kernel: algorithmic bytes per launch / average launch time
     read_bytes = B * (4 * m * k + 4 * m + 4 + 4) + 4
@@ -439,10 +444,11 @@ def main():
         "metric": METRIC, "value": value, "unit": "unit-props/s" if capped else "instances/s", "n_gpus": world, "steps": args.steps,
         "warmup": warm, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int32",
-        "data": "synthetic: uniform random k-SAT generated in HBM (seeded), 2 batches alternated on 2 streams",
+        "data": f"synthetic: uniform random k-SAT generated in HBM (seeded), {NS} batches rotated on {NS} streams",
         "config": {"workload": desc, "preset": args.workload, "node_limit": args.node_limit,
                    "instances_per_step": args.total, "instances_per_gpu": B, "n": n, "m": m, "k": k,
-                   "parallelism": f"instance-sharded x{world}"},
+                   "parallelism": f"instance-sharded x{world}", "streams": NS,
+                   "branch_splitting": not args.no_split},
         "instances_per_s": all_inst / elapsed,
         "unit_props_per_s": props / elapsed,
         "capped_fraction": int(((status == 2).sum()).item()) / B,

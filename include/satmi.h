@@ -186,6 +186,16 @@ uint64_t satmi_dpll_scan_lds_bytes(int max_vars, int max_clauses, int max_lits, 
 #define SATMI_KERNEL_INC 3
 int satmi_dpll_set_kernel(int policy);
 
+/* Branch splitting in the clause kernels (process-wide; default on): once a
+ * launch's instance queue drains, idle wavefronts take over the False branches
+ * of open decisions of the searches still running (a search checks for idle
+ * wavefronts every 16 decisions); the donor takes the helper's result when its
+ * backtracking reaches the branch.  Statuses, counters and models are those of
+ * the unsplit search (branches a sequential search would not have visited are
+ * cancelled and count nothing).  Applies to SOUND-mode launches with
+ * max_solutions == 1, no node limit and no time limit. */
+int satmi_dpll_set_split(int enable);
+
 /* The launch satmi_dpll_batch_device would make for this batch shape under the
  * current policy: *kernel = SATMI_KERNEL_SCAN or SATMI_KERNEL_GENERAL, LDS
  * bytes per wavefront, and wavefronts resident per CU (LDS and registers). */

@@ -1022,7 +1022,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     // the row's tick count collects helpers' busy time minus time spent waiting
     // on them; the wave's own elapsed time is added at the end
     if (A.split && ln == 0) st_agent(&ctr[SATMI_CTR_TICKS], (int64_t)0);
-    if (!is_task) {
+    if (true) {
         // root snapshot: the input's unit clauses in order (no clause is empty yet)
         int root_empty = INT_MAX;   // no clause is empty before any assignment
         nu = scan_units<K>(S, mpad, ep, 0u, &root_empty);
@@ -1214,7 +1214,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     if (nd > 0) cancel_donations(A, dst, nd);   // a model (or a cancellation) came first
     flush_counters(ctr, c, flushed);
     const int64_t ticks = (int64_t)(__builtin_amdgcn_s_memrealtime() - t_start);
-    if (is_task) {
+    if (false) {
         const SlotRef me = slot_ref(A, task);
         if (ln == 0) {
             st_agent(&me.h->status, status);
@@ -1233,7 +1233,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
 // An idle wave's next donated subtree: {instance, slot}, or y < 0 once every
 // instance of the launch has finished.  Not inlined: its polling addresses
 // would otherwise be hoisted into registers held across the node loop.
-__device__ __forceinline__ int2 next_donation(SplitCfg *cfg, int num_instances) {
+__device__ __attribute__((noinline)) int2 next_donation(SplitCfg *cfg, int num_instances) {
     const int ln = lane_id();
     for (;;) {
         if (uniform_u32(ld_agent(&cfg->ctl.done)) >= (uint32_t)num_instances) return make_int2(-1, -1);
@@ -1289,8 +1289,7 @@ __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) 
             b = w.x;
             task = w.y;
         }
-        // wave-uniform (a divergent-looking b costs 64-bit VGPR address math)
-        solve_instance<K, INC, C>(A, S, uniform_i32(b), uniform_i32(task), dst);
+        solve_instance<K, INC, C>(A, S, b, task, dst);
         if (A.split && ln == 0) add_agent(task < 0 ? (int32_t *)&A.split->ctl.done : &A.split->ctl.want, 1);
         wave_sync();
     }

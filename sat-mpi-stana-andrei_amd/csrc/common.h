@@ -23,6 +23,14 @@ int hip_fail(hipError_t e, const char *what);
 // One CDNA wavefront = 64 lanes.  The DPLL kernel runs one instance per wave;
 // control flow is wave-uniform and lanes cooperate on clause / variable scans.
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+// The same, recomputed where it is written: for rarely taken paths inside hot
+// loops, so the compiler cannot hoist lane-dependent addresses of the rare
+// path out of the loop (hoisted, they hold VGPRs across the whole loop).
+__device__ __forceinline__ int lane_id_here() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const int l = lane_id();

@@ -882,12 +882,17 @@ struct DeviceWork {
     std::unordered_map<hipStream_t, uint32_t *> counters;
     // incremental scan kernel: occurrence-list scratch per stream (grown, never shrunk)
     std::unordered_map<hipStream_t, std::pair<uint16_t *, size_t>> occ;
+    // branch splitting: slot pool + donation stacks per stream (grown, never
+    // shrunk) and the stream's launch tag for the slot states
+    std::unordered_map<hipStream_t, std::pair<void *, size_t>> split;
+    std::unordered_map<hipStream_t, uint32_t> split_epoch;
     double ticks_per_s = 1e8;
     bool init = false;
 };
 static std::mutex g_work_mu;
 static std::vector<DeviceWork> g_work;
 static std::atomic<int> g_kernel_policy{SATMI_KERNEL_AUTO};
+static std::atomic<int> g_split_enable{1};
 
 static int device_work(hipStream_t stream, DeviceWork **out, uint32_t **counter) {
     int dev = 0;
@@ -960,6 +965,41 @@ static uint16_t *occ_scratch(hipStream_t stream, size_t bytes) {
     }
     slot = {(uint16_t *)p, bytes};
     return slot.first;
+}
+
+// Branch-splitting scratch on `stream` (same lifetime rule as occ_scratch) and
+// the next launch tag of its slot states.
+static void *split_scratch(hipStream_t stream, size_t bytes, uint32_t *epoch) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_work_mu);
+    if ((int)g_work.size() <= dev) g_work.resize(dev + 1);
+    auto &slot = g_work[dev].split[stream];
+    uint32_t &ep = g_work[dev].split_epoch[stream];
+    if (slot.second < bytes) {
+        if (slot.first) {
+            if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+            (void)hipFree(slot.first);
+            slot = {nullptr, 0};
+        }
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            set_error("branch-splitting scratch: hipMalloc failed");
+            return nullptr;
+        }
+        // fresh memory: no stale state may carry the next tags
+        if (hipMemsetAsync(p, 0, bytes, stream) != hipSuccess) return nullptr;
+        slot = {p, bytes};
+    }
+    ep = (ep + 1u) & 0x0FFFFFFFu;
+    if (ep == 0u) ep = 1u;
+    *epoch = ep;
+    return slot.first;
+}
+
+extern "C" int satmi_dpll_set_split(int enable) {
+    g_split_enable.store(enable ? 1 : 0);
+    return SATMI_OK;
 }
 
 extern "C" int satmi_dpll_set_kernel(int policy) {
@@ -1089,6 +1129,12 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         Lc.stream = (hipStream_t)stream;
         Lc.inc = inc;
         Lc.occ_alloc = [stream](size_t bytes) { return occ_scratch((hipStream_t)stream, bytes); };
+        // branch splitting reproduces the sequential search exactly only when
+        // the search stops at its first model and nothing else cuts it short
+        Lc.split = g_split_enable.load() && max_solutions == 1 && node_limit <= 0 && time_limit_s <= 0;
+        Lc.split_alloc = [stream](size_t bytes, uint32_t *epoch) {
+            return split_scratch((hipStream_t)stream, bytes, epoch);
+        };
         SATMI_HIP(hipMemsetAsync(wc, 0, 24, Lc.stream));   // counter + launch span (common.h)
         return dpll_scan_launch(Lc);
     }

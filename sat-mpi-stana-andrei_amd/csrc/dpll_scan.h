@@ -25,6 +25,12 @@ struct ScanLaunch {
     // incremental kernel: returns >= bytes of device scratch for the occurrence lists,
     // valid for this launch on `stream` (nullptr on failure)
     std::function<uint16_t *(size_t)> occ_alloc;
+    // branch splitting of the launch's tail (dpll_scan.hip, "Splitting the tail"):
+    // split_alloc returns >= bytes of device scratch valid for this launch on
+    // `stream` and the launch's tag for the slot states (distinct per launch on
+    // the stream), nullptr on failure
+    bool split = false;
+    std::function<void *(size_t, uint32_t *)> split_alloc;
 };
 
 // Can the scan kernel take a batch of this shape (SOUND mode, no caller

@@ -29,13 +29,18 @@ EXPORTED = (
     "satmi_dpll_batch_device", "satmi_dpll_batch_host", "satmi_dpll_lds_bytes", "satmi_resolution_host",
     "satmi_dp_host", "satmi_dpll_scan_lds_bytes", "satmi_dpll_set_kernel", "satmi_dpll_plan",
     "satmi_dpll_launch_span", "satmi_wallclock_hz", "satmi_resolution_debug_slot_base",
-    "satmi_resolution_last_stats",
+    "satmi_resolution_last_stats", "satmi_dpll_set_split",
 )
 
 
 def set_kernel(policy):
     """Process-wide DPLL kernel policy (KERNEL_AUTO / KERNEL_GENERAL / KERNEL_SCAN / KERNEL_INC)."""
     check(load().satmi_dpll_set_kernel(int(policy)), "satmi_dpll_set_kernel")
+
+
+def set_split(enable):
+    """Process-wide branch splitting of the clause kernels' launch tails (default on)."""
+    check(load().satmi_dpll_set_split(int(bool(enable))), "satmi_dpll_set_split")
 
 
 class SatmiError(RuntimeError):
@@ -76,6 +81,7 @@ def load():
     L.satmi_dpll_scan_lds_bytes.restype = ctypes.c_uint64
     L.satmi_dpll_scan_lds_bytes.argtypes = [ctypes.c_int] * 4
     L.satmi_dpll_set_kernel.argtypes = [ctypes.c_int]
+    L.satmi_dpll_set_split.argtypes = [ctypes.c_int]
     L.satmi_dpll_launch_span.argtypes = [vp, vp]
     L.satmi_wallclock_hz.argtypes = [P(ctypes.c_double)]
     L.satmi_dpll_plan.argtypes = [ctypes.c_int] * 6 + [P(ctypes.c_int), P(ctypes.c_uint64), P(ctypes.c_int)]

@@ -363,3 +363,44 @@ def test_scan_kernel_chunk_group_tails(n, m, cap):
         for key in CTR:
             assert rs.counter_dict(b)[key] == o["counters"][key], (b, key)
         assert rs.solutions(b)[:1] == o["solutions"][:1]
+
+
+def _run_split(batch, split, policy=_capi.KERNEL_AUTO, **kw):
+    _capi.set_split(split)
+    try:
+        return _run_policy(batch, policy, **kw)
+    finally:
+        _capi.set_split(True)
+
+
+@pytest.mark.parametrize("n,m,B,policy", [(100, 426, 24, _capi.KERNEL_AUTO), (100, 426, 3000, _capi.KERNEL_AUTO),
+                                          (50, 213, 40, _capi.KERNEL_AUTO), (140, 596, 16, _capi.KERNEL_INC),
+                                          (100, 426, 24, _capi.KERNEL_SCAN)])
+def test_branch_splitting_matches_unsplit(n, m, B, policy):
+    """Branch splitting (dpll_scan.hip, "Splitting the tail"): a batch far
+    smaller than the resident waves makes nearly every search donate subtrees
+    to idle waves (and helpers donate further); statuses, every counter and
+    the models must equal the unsplit search, and the oracle on a sample."""
+    batch = cnf.uniform_ksat(B, n, m, 3, seed=n * B + m)
+    ru = _run_split(batch, False, policy, max_solutions=1, sol_cap=1)
+    rs = _run_split(batch, True, policy, max_solutions=1, sol_cap=1)
+    assert (rs.status == ru.status).all()
+    assert (rs.counters[:, :7] == ru.counters[:, :7]).all()
+    assert (rs.sol_len == ru.sol_len).all()
+    assert (rs.sol_lits == ru.sol_lits).all()
+    for b in range(0, B, max(1, B // 6)):
+        o = oracle.dpll(batch.instance(b), "sound", max_solutions=1, sol_cap=1)
+        for key in CTR:
+            assert rs.counter_dict(b)[key] == o["counters"][key], (b, key)
+        assert rs.solutions(b)[:1] == o["solutions"][:1]
+
+
+def test_branch_splitting_repeated_launches_one_stream():
+    """Slot states are tagged per launch (the pool is never cleared): many
+    back-to-back split launches on one stream stay exact."""
+    batch = cnf.uniform_ksat(32, 100, 426, 3, seed=99)
+    ru = _run_split(batch, False, max_solutions=1, sol_cap=1)
+    for _ in range(6):
+        rs = _run_split(batch, True, max_solutions=1, sol_cap=1)
+        assert (rs.counters[:, :7] == ru.counters[:, :7]).all()
+        assert (rs.sol_lits == ru.sol_lits).all()
