@@ -174,16 +174,20 @@ uint64_t satmi_dpll_scan_lds_bytes(int max_vars, int max_clauses, int max_lits, 
 
 /* Which DPLL kernel satmi_dpll_batch_* use (process-wide; default AUTO):
  *   AUTO     the incremental clause kernel where eligible, else the general kernel
+ *            (its wide HBM-arena form when the batch exceeds the LDS layout)
  *   GENERAL  always the general (occurrence-list, clause-counter) kernel
  *   SCAN     the clause-scan kernel, every propagation round a full clause scan;
  *            an ineligible call fails with SATMI_ERR_ARG
  *   INC      the clause kernel with incremental rounds (only the clauses that lost
  *            a literal are read); an ineligible call fails with SATMI_ERR_ARG
- * All four give identical statuses, counters and models. */
+ *   WIDE     the general kernel in its wide form (see SATMI_KERNEL_WIDE)
+ * All give identical statuses, counters and models. */
 #define SATMI_KERNEL_AUTO 0
 #define SATMI_KERNEL_GENERAL 1
 #define SATMI_KERNEL_SCAN 2
 #define SATMI_KERNEL_INC 3
+#define SATMI_KERNEL_WIDE 4   /* the general kernel with its image in a per-wave HBM arena (32-bit
+                                 indices); AUTO takes it for batches beyond the LDS layout */
 int satmi_dpll_set_kernel(int policy);
 
 /* Branch splitting in the clause kernels (process-wide; default on): once a

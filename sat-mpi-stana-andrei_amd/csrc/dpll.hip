@@ -54,12 +54,54 @@ namespace satmi {
 
 constexpr uint32_t VS_ASSIGNED = 1u, VS_VALUE = 2u, VS_EFF = 4u, VS_FLAGS = 7u;
 constexpr int VS_TIME_SHIFT = 3;
-constexpr uint32_t PHASE_BIT = 0x8000u;
-// cst[c] = nfree | ntrue << 8 | (sum of the free literal codes mod 2^16) << 16:
-// when nfree == 1 the high half is the one free literal (clauses <= 255 literals)
-constexpr uint32_t CST_TRUE1 = 0x100u;
-constexpr uint32_t CST_NFREE = 0xFFu;
-constexpr int MAX_CLAUSE_LEN = 255;
+// Two storage widths of the same kernel (both exact REF.py semantics):
+//  * Narrow: the instance image in the wave's LDS slice; 16-bit literal codes,
+//    clause indices and literal positions; cst[c] = nfree | ntrue << 8 | (sum
+//    of the free literal codes mod 2^16) << 16 -- when nfree == 1 the high half
+//    is the one free literal (clauses <= 255 literals); cnt = pos | neg << 16.
+//  * Wide: the image in a per-wave HBM arena (L2 caches the hot part), for
+//    formulas beyond one wave's LDS (the reference's own 1000 x 50 and 5000 x 500
+//    menu runs, rezultat.txt:248-250 and :488-490); 32-bit codes / indices /
+//    positions, cst = nfree | ntrue << 16 | code sum << 32 (clauses <= 65535
+//    literals), cnt = pos | neg << 32.
+struct Narrow {
+    using Idx = uint16_t;
+    using Cst = uint32_t;
+    using Cnt = uint32_t;
+    static constexpr uint32_t PHASE = 0x8000u;   // fvar: the False branch runs
+    static constexpr int NT_SHIFT = 8, SUM_SHIFT = 16, CNT_SHIFT = 16;
+    static constexpr int MAX_LEN = 255;
+};
+struct Wide {
+    using Idx = uint32_t;
+    using Cst = uint64_t;
+    using Cnt = uint64_t;
+    static constexpr uint32_t PHASE = 0x80000000u;
+    static constexpr int NT_SHIFT = 16, SUM_SHIFT = 32, CNT_SHIFT = 32;
+    static constexpr int MAX_LEN = 65535;
+};
+template <typename T> __device__ __forceinline__ typename T::Cst cst_true1() { return (typename T::Cst)1 << T::NT_SHIFT; }
+template <typename T> __device__ __forceinline__ uint32_t cst_nfree(typename T::Cst s) {
+    return (uint32_t)(s & (((typename T::Cst)1 << T::NT_SHIFT) - 1));
+}
+template <typename T> __device__ __forceinline__ uint32_t cst_ntrue(typename T::Cst s) {
+    return (uint32_t)((s >> T::NT_SHIFT) & (((typename T::Cst)1 << (T::SUM_SHIFT - T::NT_SHIFT)) - 1));
+}
+// nfree == 1 and ntrue == 0: a unit clause of the reduced formula
+template <typename T> __device__ __forceinline__ bool cst_unit(typename T::Cst s) {
+    return (s & (((typename T::Cst)1 << T::SUM_SHIFT) - 1)) == 1;
+}
+template <typename T> __device__ __forceinline__ uint32_t cst_sum(typename T::Cst s) {
+    return (uint32_t)(s >> T::SUM_SHIFT);
+}
+// one occurrence of a positive (negative) literal in a cnt word
+template <typename T> __device__ __forceinline__ typename T::Cnt cnt_one(uint32_t code) {
+    return (code & 1u) ? ((typename T::Cnt)1 << T::CNT_SHIFT) : (typename T::Cnt)1;
+}
+template <typename T> __device__ __forceinline__ uint32_t cnt_pos(typename T::Cnt c) {
+    return (uint32_t)(c & (((typename T::Cnt)1 << T::CNT_SHIFT) - 1));
+}
+template <typename T> __device__ __forceinline__ uint32_t cnt_neg(typename T::Cnt c) { return (uint32_t)(c >> T::CNT_SHIFT); }
 constexpr uint32_t NO_CLAIM = 0xFFFFFFFFu;
 
 // Diagnostic build only (make diag -> libsatmi_diag.so): per-phase shader-clock
@@ -119,29 +161,30 @@ struct DpllArgs {
     DpllLayout lay;
 };
 
-struct Lds {
-    uint16_t *lit;      // [lcap]      literal codes, clause-major (REF.py's clause lists)
-    uint16_t *coff;     // [mcap+1]    clause offsets into lit
-    uint16_t *occoff;   // [2ncap+3]   occurrence-list offsets per literal code
-    uint16_t *occ;      // [lcap]      clause index of every occurrence, grouped by literal code
-    uint32_t *cst;      // [mcap]      nfree | ntrue << 8 | free-literal code sum << 16
-    uint32_t *vst;      // [ncap+1]    assigned / value / effective bits, batch time + 1 above bit 3
-    uint32_t *cnt;      // [ncap+1]    occurrences in active clauses: positive | negative << 16
-    uint32_t *claim;    // [ncap+1]    first snapshot index claiming the variable (scratch)
-    uint16_t *trail;    // [ncap+1]    assignment order (literal codes) == dict insertion order
-    uint16_t *fvar;     // [ncap+1]    decision frames: var | PHASE_BIT once the False branch runs
-    uint16_t *ftrail;   // [ncap+1]    trail length before the decision
-    uint16_t *units;    // [mcap+1]    current unit-clause snapshot (literal codes)
-    uint64_t *ubits;    // [mcap/64]   clauses that became unit in the current batch
-    uint64_t *posbits;  // [lcap/64]   pure literals by first position
-    int32_t *mark;      // [64]        scratch row (range starts of a flattened apply)
+template <typename T>
+struct LdsT {
+    using Idx = typename T::Idx;
+    Idx *lit;                  // [lcap]      literal codes, clause-major (REF.py's clause lists)
+    Idx *coff;                 // [mcap+1]    clause offsets into lit
+    Idx *occoff;               // [2ncap+3]   occurrence-list offsets per literal code
+    Idx *occ;                  // [lcap]      clause index of every occurrence, grouped by literal code
+    typename T::Cst *cst;      // [mcap]      nfree | ntrue | free-literal code sum (see Narrow / Wide)
+    uint32_t *vst;             // [ncap+1]    assigned / value / effective bits, batch time + 1 above bit 3
+    typename T::Cnt *cnt;      // [ncap+1]    occurrences in active clauses: positive | negative
+    typename T::Cnt *claim;    // [ncap+1]    first snapshot index claiming the variable (scratch; cursor at staging)
+    Idx *trail;                // [ncap+1]    assignment order (literal codes) == dict insertion order
+    Idx *fvar;                 // [ncap+1]    decision frames: var | T::PHASE once the False branch runs
+    Idx *ftrail;               // [ncap+1]    trail length before the decision
+    Idx *units;                // [mcap+1]    current unit-clause snapshot (literal codes)
+    uint64_t *ubits;           // [mcap/64]   clauses that became unit in the current batch
+    uint64_t *posbits;         // [lcap/64]   pure literals by first position
+    int32_t *mark;             // [64]        scratch row (range starts of a flattened apply)
 };
-
-__device__ __forceinline__ uint32_t cst_ntrue(uint32_t s) { return (s >> 8) & 0xFFu; }
 
 // Time stamp of the clause's emptying: the latest batch time among its (all
 // false) literals.
-__device__ int emptied_time(const Lds &S, uint32_t c) {
+template <typename T>
+__device__ int emptied_time(const LdsT<T> &S, uint32_t c) {
     int t = -1;
     const int je = S.coff[c + 1];
     for (int j = S.coff[c]; j < je; ++j) t = max(t, (int)(S.vst[S.lit[j] >> 1] >> VS_TIME_SHIFT) - 1);
@@ -151,8 +194,8 @@ __device__ int emptied_time(const Lds &S, uint32_t c) {
 // A clause leaves (UNDO: re-enters) the reduced formula: its literals' active
 // occurrence counts change.  Slots past the clause end add 0 to cnt[0] (an
 // unused word) so the group of four loads and atomics runs without branches.
-template <bool UNDO>
-__device__ __forceinline__ void clause_counts(const Lds &S, uint32_t c) {
+template <typename T, bool UNDO>
+__device__ __forceinline__ void clause_counts(const LdsT<T> &S, uint32_t c) {
     const int jb = S.coff[c], je = S.coff[c + 1];
     for (int j = jb; j < je; j += 4) {
         uint32_t x[4];
@@ -161,7 +204,7 @@ __device__ __forceinline__ void clause_counts(const Lds &S, uint32_t c) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const bool in = j + u < je;
-            const uint32_t inc = in ? ((x[u] & 1u) ? 0x10000u : 1u) : 0u;
+            const typename T::Cnt inc = in ? cnt_one<T>(x[u]) : (typename T::Cnt)0;
             const uint32_t v = in ? (x[u] >> 1) : 0u;
             if (UNDO) atomicAdd(&S.cnt[v], inc);
             else atomicSub(&S.cnt[v], inc);
@@ -172,22 +215,23 @@ __device__ __forceinline__ void clause_counts(const Lds &S, uint32_t c) {
 // One occurrence of literal `code` (r < n0: in its own list, else in its
 // negation's list), as one atomic on the clause word.  Returns true when the
 // clause changed satisfied state.
-template <bool UNDO>
-__device__ __forceinline__ bool occ_step(const Lds &S, int r, int n0, int b0, int b1, uint32_t code, int &e_loc) {
+template <typename T, bool UNDO>
+__device__ __forceinline__ bool occ_step(const LdsT<T> &S, int r, int n0, int b0, int b1, uint32_t code, int &e_loc) {
     const bool pos = r < n0;
     const uint32_t c = S.occ[pos ? b0 + r : b1 + (r - n0)];
     // own list: a true occurrence more (undo: less); negation's list: a free
     // occurrence less and its code leaves the sum (undo: back)
-    const uint32_t fdelta = 1u + ((code ^ 1u) << 16);
-    const uint32_t delta = pos ? (UNDO ? 0u - CST_TRUE1 : CST_TRUE1) : (UNDO ? fdelta : 0u - fdelta);
-    const uint32_t old = atomicAdd(&S.cst[c], delta);
-    const bool trans = pos && cst_ntrue(old) == (UNDO ? 1u : 0u);
-    if (trans) clause_counts<UNDO>(S, c);
+    using Cst = typename T::Cst;
+    const Cst fdelta = (Cst)1 + ((Cst)(code ^ 1u) << T::SUM_SHIFT);
+    const Cst delta = pos ? (UNDO ? (Cst)0 - cst_true1<T>() : cst_true1<T>()) : (UNDO ? fdelta : (Cst)0 - fdelta);
+    const Cst old = atomicAdd(&S.cst[c], delta);
+    const bool trans = pos && cst_ntrue<T>(old) == (UNDO ? 1u : 0u);
+    if (trans) clause_counts<T, UNDO>(S, c);
     if (!UNDO && !pos) {
-        const uint32_t nf = (old & CST_NFREE) - 1u;
+        const uint32_t nf = cst_nfree<T>(old) - 1u;
         if (nf == 0u) {
             e_loc = min(e_loc, emptied_time(S, c));
-        } else if (nf == 1u && cst_ntrue(old) == 0u) {
+        } else if (nf == 1u && cst_ntrue<T>(old) == 0u) {
             atomicOr((unsigned long long *)&S.ubits[c >> 6], 1ull << (c & 63));
         }
     }
@@ -202,8 +246,8 @@ __device__ __forceinline__ bool occ_step(const Lds &S, int r, int n0, int b0, in
 // its owner lane by marking range starts and a max-scan).  Returns the change
 // in the number of satisfied clauses; on apply, e_loc collects the time stamps
 // of emptied clauses and newly-unit clauses are flagged in ubits.
-template <bool UNDO>
-__device__ int apply_lanes(const Lds &S, bool has, uint32_t code, int &e_loc) {
+template <typename T, bool UNDO>
+__device__ int apply_lanes(const LdsT<T> &S, bool has, uint32_t code, int &e_loc) {
     const int ln = lane_id();
     int b0 = 0, n0 = 0, b1 = 0, len = 0;
     if (has) {
@@ -223,7 +267,7 @@ __device__ int apply_lanes(const Lds &S, bool has, uint32_t code, int &e_loc) {
         for (int f0 = 0; f0 < olen; f0 += 64) {
             const int f = f0 + ln;
             bool trans = false;
-            if (f < olen) trans = occ_step<UNDO>(S, f, on0, ob0, ob1, ocode, e_loc);
+            if (f < olen) trans = occ_step<T, UNDO>(S, f, on0, ob0, ob1, ocode, e_loc);
             dsat += __popcll(__ballot(trans));
         }
     } else {
@@ -247,7 +291,7 @@ __device__ int apply_lanes(const Lds &S, bool has, uint32_t code, int &e_loc) {
             const int ob1 = __shfl(b1, o, 64);
             const uint32_t ocode = (uint32_t)__shfl((int)code, o, 64);
             bool trans = false;
-            if (f < total) trans = occ_step<UNDO>(S, r, on0, ob0, ob1, ocode, e_loc);
+            if (f < total) trans = occ_step<T, UNDO>(S, r, on0, ob0, ob1, ocode, e_loc);
             dsat += __popcll(__ballot(trans));
         }
     }
@@ -256,8 +300,8 @@ __device__ int apply_lanes(const Lds &S, bool has, uint32_t code, int &e_loc) {
 }
 
 // apply_lanes over trail[beg, end) (UNDO: only the effective entries).
-template <bool UNDO>
-__device__ int apply_trail(const Lds &S, int beg, int end) {
+template <typename T, bool UNDO>
+__device__ int apply_trail(const LdsT<T> &S, int beg, int end) {
     int dsat = 0, e_loc = INT_MAX;
     for (int e0 = beg; e0 < end; e0 += 64) {
         const int e = e0 + lane_id();
@@ -267,19 +311,21 @@ __device__ int apply_trail(const Lds &S, int beg, int end) {
             code = S.trail[e];
             has = !UNDO || (S.vst[code >> 1] & VS_EFF);
         }
-        dsat += apply_lanes<UNDO>(S, has, code, e_loc);
+        dsat += apply_lanes<T, UNDO>(S, has, code, e_loc);
     }
     return dsat;
 }
 
-__device__ void clear_ubits(const Lds &S, int m) {
+template <typename T>
+__device__ void clear_ubits(const LdsT<T> &S, int m) {
     for (int w = lane_id(); w < ((m + 63) >> 6); w += 64) S.ubits[w] = 0ull;
     wave_sync();
 }
 
 // The next snapshot: clauses flagged in ubits that are still unit, in clause
 // order (REF.py:143); cst's high half holds the one free literal's code.
-__device__ int collect_units(const Lds &S, int m) {
+template <typename T>
+__device__ int collect_units(const LdsT<T> &S, int m) {
     const int ln = lane_id();
     const int W = (m + 63) >> 6;
     int nu = 0;
@@ -293,14 +339,14 @@ __device__ int collect_units(const Lds &S, int m) {
         uint64_t keep = 0;
         for (uint64_t b = bits; b; b &= b - 1) {
             const int c = w * 64 + (__ffsll((unsigned long long)b) - 1);
-            if ((S.cst[c] & 0xFFFFu) == 1u) keep |= b & (~b + 1);   // nfree == 1, ntrue == 0
+            if (cst_unit<T>(S.cst[c])) keep |= b & (~b + 1);   // nfree == 1, ntrue == 0
         }
         const int kc = __popcll(keep);
         const int incl = wave_incl_scan(kc);
         int pos = nu + incl - kc;
         for (; keep; keep &= keep - 1) {
             const int c = w * 64 + (__ffsll((unsigned long long)keep) - 1);
-            S.units[pos++] = (uint16_t)(S.cst[c] >> 16);
+            S.units[pos++] = (typename T::Idx)cst_sum<T>(S.cst[c]);
         }
         nu += lane63(incl);
     }
@@ -311,7 +357,8 @@ __device__ int collect_units(const Lds &S, int m) {
 // unit_propagate (REF.py:139-165) from the snapshot S.units[0, nu).  Returns
 // true on conflict.  `trail_len` ends at the exact point the reference stops
 // (the assignments it made, including the one that emptied a clause).
-__device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, int nu, bool decision_round,
+template <typename T>
+__device__ bool propagate(const LdsT<T> &S, int m, bool has_empty, int &trail_len, int nu, bool decision_round,
                           int64_t &props, int64_t &rounds, int &nsat, PhaseClock &ph) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
@@ -337,14 +384,14 @@ __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, i
             // the first occurrence of each unassigned variable before the mismatch
             // is assigned, time-stamped with its snapshot index (REF.py:154)
             const bool claimable = valid && !assigned && k < kmis;
-            if (claimable) atomicMin(&S.claim[v], (uint32_t)k);
+            if (claimable) atomicMin(&S.claim[v], (typename T::Cnt)k);
             wave_sync();
-            first = claimable && S.claim[v] == (uint32_t)k;
+            first = claimable && S.claim[v] == (typename T::Cnt)k;
             wave_sync();
             if (claimable) S.claim[v] = NO_CLAIM;
             const uint64_t mk = __ballot(first);
             if (first) {
-                S.trail[trail_len + __popcll(mk & lt)] = (uint16_t)code;
+                S.trail[trail_len + __popcll(mk & lt)] = (typename T::Idx)code;
                 S.vst[v] = VS_ASSIGNED | VS_EFF | ((code & 1u) ? 0u : VS_VALUE) |
                            ((uint32_t)(k + 1) << VS_TIME_SHIFT);
             }
@@ -354,7 +401,7 @@ __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, i
             PH_MARK(PH_ASSIGN);
             // reduce the formula by this part of the batch (REF.py:156-164)
             int e_loc = INT_MAX;
-            nsat += apply_lanes<false>(S, first, code, e_loc);
+            nsat += apply_lanes<T, false>(S, first, code, e_loc);
             e_min = wave_min_i32(e_loc);
             if (has_empty && mk) e_min = min(e_min, first_k);   // `[]` empties at the first reduction
             PH_MARK(PH_APPLY);
@@ -370,7 +417,7 @@ __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, i
                 keep += __popcll(__ballot(p));
             }
             const int cut = round_start + keep;
-            nsat += apply_trail<true>(S, cut, trail_len);
+            nsat += apply_trail<T, true>(S, cut, trail_len);
             for (int i = round_start + ln; i < trail_len; i += 64) {
                 const uint32_t v = S.trail[i] >> 1;
                 S.vst[v] = i < cut ? (S.vst[v] & VS_FLAGS) : 0u;
@@ -404,14 +451,15 @@ __device__ bool propagate(const Lds &S, int m, bool has_empty, int &trail_len, i
 // key of literal_sign / var_counts' dict order (REF.py:174-179, :198-203).
 // Occurrence lists are sorted by clause, so each walk stops at its first
 // active clause.  Requires v to occur in an active clause.
-__device__ uint32_t first_position(const Lds &S, uint32_t v) {
+template <typename T>
+__device__ uint32_t first_position(const LdsT<T> &S, uint32_t v) {
     uint32_t best = 0xFFFFFFFFu;
     for (uint32_t code = v << 1; code <= ((v << 1) | 1u); ++code) {
         const int e = S.occoff[code + 1];
         for (int i = S.occoff[code]; i < e; ++i) {
             const uint32_t c = S.occ[i];
             if (c >= best) break;
-            if (cst_ntrue(S.cst[c]) == 0u) {
+            if (cst_ntrue<T>(S.cst[c]) == 0u) {
                 best = c;
                 break;
             }
@@ -430,7 +478,8 @@ struct AnRes {
 };
 
 // literal_sign / pure_literals / var_counts (REF.py:174-208).
-__device__ AnRes analyze(const Lds &S, int n) {
+template <typename T>
+__device__ AnRes analyze(const LdsT<T> &S, int n) {
     const int ln = lane_id();
     int npure = 0;
     uint32_t maxc = 0;
@@ -438,8 +487,8 @@ __device__ AnRes analyze(const Lds &S, int n) {
         const int v = v0 + ln;
         bool pure = false;
         if (v <= n && !(S.vst[v] & VS_ASSIGNED)) {
-            const uint32_t c = S.cnt[v];
-            const uint32_t p = c & 0xFFFFu, q = c >> 16;
+            const typename T::Cnt c = S.cnt[v];
+            const uint32_t p = cnt_pos<T>(c), q = cnt_neg<T>(c);
             if (p + q) {
                 maxc = max(maxc, p + q);
                 if (p == 0u || q == 0u) {
@@ -459,8 +508,8 @@ __device__ AnRes analyze(const Lds &S, int n) {
     for (int v0 = 1; v0 <= n; v0 += 64) {
         const int v = v0 + ln;
         if (v <= n && !(S.vst[v] & VS_ASSIGNED)) {
-            const uint32_t c = S.cnt[v];
-            if ((c & 0xFFFFu) + (c >> 16) == maxc) bestf = min(bestf, first_position(S, (uint32_t)v));
+            const typename T::Cnt c = S.cnt[v];
+            if (cnt_pos<T>(c) + cnt_neg<T>(c) == maxc) bestf = min(bestf, first_position(S, (uint32_t)v));
         }
     }
     bestf = wave_min_u32(bestf);
@@ -468,7 +517,8 @@ __device__ AnRes analyze(const Lds &S, int n) {
 }
 
 // Append the pure literals to the trail in first-occurrence order (REF.py:187-189).
-__device__ int assign_pures(const Lds &S, int L, int trail_len) {
+template <typename T>
+__device__ int assign_pures(const LdsT<T> &S, int L, int trail_len) {
     const int ln = lane_id();
     const int W = (L + 63) >> 6;
     int base = 0;
@@ -483,8 +533,8 @@ __device__ int assign_pures(const Lds &S, int L, int trail_len) {
             bits &= bits - 1;
             const uint32_t p = (uint32_t)(w * 64 + bit);
             const uint32_t v = S.lit[p] >> 1;
-            const bool positive = (S.cnt[v] & 0xFFFFu) != 0u;
-            S.trail[pos++] = (uint16_t)((v << 1) | (positive ? 0u : 1u));
+            const bool positive = cnt_pos<T>(S.cnt[v]) != 0u;
+            S.trail[pos++] = (typename T::Idx)((v << 1) | (positive ? 0u : 1u));
             S.vst[v] = VS_ASSIGNED | VS_EFF | (positive ? VS_VALUE : 0u);
         }
         if (w < W) S.posbits[w] = 0ull;
@@ -494,7 +544,8 @@ __device__ int assign_pures(const Lds &S, int L, int trail_len) {
     return trail_len + uniform_i32(base);
 }
 
-__device__ void store_assignment(const Lds &S, int trail_len, int32_t *out) {
+template <typename T>
+__device__ void store_assignment(const LdsT<T> &S, int trail_len, int32_t *out) {
     for (int i = lane_id(); i < trail_len; i += 64) {
         const uint32_t code = S.trail[i];
         const int v = (int)(code >> 1);
@@ -503,15 +554,17 @@ __device__ void store_assignment(const Lds &S, int trail_len, int32_t *out) {
 }
 
 // Pop trail[ft, trail_len): revert the effective ones, clear every variable.
-__device__ void unassign_to(const Lds &S, int ft, int trail_len, int &nsat) {
-    nsat += apply_trail<true>(S, ft, trail_len);
+template <typename T>
+__device__ void unassign_to(const LdsT<T> &S, int ft, int trail_len, int &nsat) {
+    nsat += apply_trail<T, true>(S, ft, trail_len);
     for (int i = ft + lane_id(); i < trail_len; i += 64) S.vst[S.trail[i] >> 1] = 0u;
     wave_sync();
 }
 
 enum { ST_PROPAGATE = 0, ST_ANALYZE = 1, ST_BACKTRACK = 2, ST_DONE = 3 };
 
-__device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
+template <typename T>
+__device__ void solve_instance(const DpllArgs &A, const LdsT<T> &S, int b) {
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     PhaseClock ph;
     ph.start();
@@ -540,9 +593,9 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
     for (int i = ln; i < L; i += 64) {
         const int x = A.lits[lb + i];
         const uint32_t v = (uint32_t)(x < 0 ? -x : x);
-        S.lit[i] = (uint16_t)((v << 1) | (x < 0 ? 1u : 0u));
+        S.lit[i] = (typename T::Idx)((v << 1) | (x < 0 ? 1u : 0u));
     }
-    for (int i = ln; i <= m; i += 64) S.coff[i] = (uint16_t)(A.clause_lit_begin[cb + i] - lb);
+    for (int i = ln; i <= m; i += 64) S.coff[i] = (typename T::Idx)(A.clause_lit_begin[cb + i] - lb);
     for (int v = ln; v <= n; v += 64) {
         S.vst[v] = 0u;
         S.cnt[v] = 0u;
@@ -551,14 +604,14 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
     for (int w = ln; w < ((m + 63) >> 6); w += 64) S.ubits[w] = 0ull;
     for (int w = ln; w < ((L + 63) >> 6); w += 64) S.posbits[w] = 0ull;
     wave_sync();
-    // cst = clause length | code sum << 16; clauses longer than 255 literals do not fit
+    // cst = clause length | code sum; clauses longer than T::MAX_LEN literals do not fit
     bool too_long = false;
     for (int c = ln; c < m; c += 64) {
         const int jb = S.coff[c], je = S.coff[c + 1];
         uint32_t sum = 0;
         for (int j = jb; j < je; ++j) sum += S.lit[j];
-        too_long |= (je - jb) > MAX_CLAUSE_LEN;
-        S.cst[c] = (uint32_t)(je - jb) | (sum << 16);
+        too_long |= (je - jb) > T::MAX_LEN;
+        S.cst[c] = (typename T::Cst)(je - jb) | ((typename T::Cst)sum << T::SUM_SHIFT);
     }
     if (__ballot(too_long)) {
         if (ln < SATMI_NCOUNTERS) ctr[ln] = 0;
@@ -570,7 +623,7 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
     }
     for (int i = ln; i < L; i += 64) {
         const uint32_t x = S.lit[i];
-        atomicAdd(&S.cnt[x >> 1], (x & 1u) ? 0x10000u : 1u);   // all clauses are active
+        atomicAdd(&S.cnt[x >> 1], cnt_one<T>(x));   // all clauses are active
     }
     wave_sync();
     // occurrence-list offsets: exclusive scan over literal codes 0 .. 2n+1
@@ -580,20 +633,20 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
             const int v = v0 + ln;
             uint32_t p = 0, q = 0;
             if (v <= n) {
-                const uint32_t c = S.cnt[v];
-                p = c & 0xFFFFu;
-                q = c >> 16;
+                const typename T::Cnt c = S.cnt[v];
+                p = cnt_pos<T>(c);
+                q = cnt_neg<T>(c);
             }
             const int tot = (int)(p + q);
             const int incl = wave_incl_scan(tot);
             if (v <= n) {
                 const int o = base + incl - tot;
-                S.occoff[2 * v] = (uint16_t)o;
-                S.occoff[2 * v + 1] = (uint16_t)(o + (int)p);
+                S.occoff[2 * v] = (typename T::Idx)o;
+                S.occoff[2 * v + 1] = (typename T::Idx)(o + (int)p);
             }
             base += lane63(incl);
         }
-        if (ln == 0) S.occoff[2 * n + 2] = (uint16_t)L;
+        if (ln == 0) S.occoff[2 * n + 2] = (typename T::Idx)L;
     }
     wave_sync();
     // scatter occurrences in position (= clause) order so every list is sorted by
@@ -611,12 +664,11 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
             grp += eq ? 1 : 0;
             rank += (eq && l < ln) ? 1 : 0;
         }
-        const uint32_t unit = (x & 1u) ? 0x10000u : 1u;
-        if (valid && rank == 0) atomicAdd(&S.claim[x >> 1], unit * (uint32_t)grp);
+        if (valid && rank == 0) atomicAdd(&S.claim[x >> 1], cnt_one<T>(x) * (typename T::Cnt)grp);
         wave_sync();
         if (valid) {
-            const uint32_t cur = S.claim[x >> 1];
-            const int after = (int)((x & 1u) ? (cur >> 16) : (cur & 0xFFFFu));
+            const typename T::Cnt cur = S.claim[x >> 1];
+            const int after = (int)((x & 1u) ? cnt_neg<T>(cur) : cnt_pos<T>(cur));
             // clause of position p: the last c with coff[c] <= p
             int lo = 0, hi = m;
             while (hi - lo > 1) {
@@ -624,7 +676,7 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                 if ((int)S.coff[mid] <= p) lo = mid;
                 else hi = mid;
             }
-            S.occ[S.occoff[x] + after - grp + rank] = (uint16_t)lo;
+            S.occ[S.occoff[x] + after - grp + rank] = (typename T::Idx)lo;
         }
         wave_sync();
     }
@@ -641,9 +693,9 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                 const uint32_t code = (v << 1) | (x < 0 ? 1u : 0u);
                 if (S.vst[v] & VS_ASSIGNED) {
                     for (int t = 0; t < tl; ++t)
-                        if ((S.trail[t] >> 1) == v) S.trail[t] = (uint16_t)code;
+                        if ((S.trail[t] >> 1) == v) S.trail[t] = (typename T::Idx)code;
                 } else {
-                    S.trail[tl++] = (uint16_t)code;
+                    S.trail[tl++] = (typename T::Idx)code;
                 }
                 S.vst[v] = VS_ASSIGNED | (x > 0 ? VS_VALUE : 0u);
             }
@@ -704,29 +756,29 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
             if (!leaf && r.npure > 0) {                       // REF.py:186-195
                 const int before = trail_len;
                 trail_len = assign_pures(S, L, trail_len);
-                nsat += apply_trail<false>(S, before, trail_len);   // a pure literal never empties a clause
+                nsat += apply_trail<T, false>(S, before, trail_len);   // a pure literal never empties a clause
                 pures += r.npure;
                 ++nodes;                                      // recursive call; its unit_propagate is a no-op
                 PH_MARK(PH_PURE);
             } else if (!leaf) {                               // REF.py:208-213
                 const uint32_t v = r.best_var;
                 if (ln == 0) {
-                    S.fvar[depth] = (uint16_t)v;
-                    S.ftrail[depth] = (uint16_t)trail_len;
+                    S.fvar[depth] = (typename T::Idx)v;
+                    S.ftrail[depth] = (typename T::Idx)trail_len;
                 }
                 ++depth;
                 ++decisions;
                 ++nodes;
                 const uint32_t code = v << 1;                 // True first
                 if (sound) {
-                    if (ln == 0) S.units[0] = (uint16_t)code;
+                    if (ln == 0) S.units[0] = (typename T::Idx)code;
                     nu = 1;
                     decision_round = true;
                     state = ST_PROPAGATE;
                 } else {
                     if (ln == 0) {
                         S.vst[v] = VS_ASSIGNED | VS_VALUE;
-                        S.trail[trail_len] = (uint16_t)code;
+                        S.trail[trail_len] = (typename T::Idx)code;
                     }
                     ++trail_len;
                 }
@@ -755,21 +807,21 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
                 const int ft = uniform_i32(S.ftrail[top]);
                 unassign_to(S, ft, trail_len, nsat);
                 trail_len = ft;
-                if (!(fv & PHASE_BIT)) {
+                if (!(fv & T::PHASE)) {
                     const uint32_t v = fv;
-                    if (ln == 0) S.fvar[top] = (uint16_t)(v | PHASE_BIT);
+                    if (ln == 0) S.fvar[top] = (typename T::Idx)(v | T::PHASE);
                     ++decisions;
                     ++nodes;
                     const uint32_t code = (v << 1) | 1u;      // False
                     if (sound) {
-                        if (ln == 0) S.units[0] = (uint16_t)code;
+                        if (ln == 0) S.units[0] = (typename T::Idx)code;
                         nu = 1;
                         decision_round = true;
                         state = ST_PROPAGATE;
                     } else {
                         if (ln == 0) {
                             S.vst[v] = VS_ASSIGNED;
-                            S.trail[trail_len] = (uint16_t)code;
+                            S.trail[trail_len] = (typename T::Idx)code;
                         }
                         ++trail_len;
                         state = ST_ANALYZE;
@@ -809,38 +861,58 @@ __device__ void solve_instance(const DpllArgs &A, const Lds &S, int b) {
 #endif
 }
 
+template <typename T>
+__device__ __forceinline__ LdsT<T> bind_storage(unsigned char *base, const DpllLayout &lay) {
+    using Idx = typename T::Idx;
+    LdsT<T> S;
+    S.lit = (Idx *)(base + lay.lit);
+    S.coff = (Idx *)(base + lay.coff);
+    S.occoff = (Idx *)(base + lay.occoff);
+    S.occ = (Idx *)(base + lay.occ);
+    S.cst = (typename T::Cst *)(base + lay.cst);
+    S.vst = (uint32_t *)(base + lay.vst);
+    S.cnt = (typename T::Cnt *)(base + lay.cnt);
+    S.claim = (typename T::Cnt *)(base + lay.claim);
+    S.trail = (Idx *)(base + lay.trail);
+    S.fvar = (Idx *)(base + lay.fvar);
+    S.ftrail = (Idx *)(base + lay.ftrail);
+    S.units = (Idx *)(base + lay.units);
+    S.ubits = (uint64_t *)(base + lay.ubits);
+    S.posbits = (uint64_t *)(base + lay.posbits);
+    S.mark = (int32_t *)(base + lay.mark);
+    return S;
+}
+
 // Persistent grid: every wave pulls instance indices from a global counter until
 // the batch is drained (instances differ wildly in search-tree size).
-__global__ void __launch_bounds__(256) dpll_batch_kernel(DpllArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int wave = threadIdx.x >> 6;
-    unsigned char *base = smem + (size_t)wave * A.lay.bytes;
-    Lds S;
-    S.lit = (uint16_t *)(base + A.lay.lit);
-    S.coff = (uint16_t *)(base + A.lay.coff);
-    S.occoff = (uint16_t *)(base + A.lay.occoff);
-    S.occ = (uint16_t *)(base + A.lay.occ);
-    S.cst = (uint32_t *)(base + A.lay.cst);
-    S.vst = (uint32_t *)(base + A.lay.vst);
-    S.cnt = (uint32_t *)(base + A.lay.cnt);
-    S.claim = (uint32_t *)(base + A.lay.claim);
-    S.trail = (uint16_t *)(base + A.lay.trail);
-    S.fvar = (uint16_t *)(base + A.lay.fvar);
-    S.ftrail = (uint16_t *)(base + A.lay.ftrail);
-    S.units = (uint16_t *)(base + A.lay.units);
-    S.ubits = (uint64_t *)(base + A.lay.ubits);
-    S.posbits = (uint64_t *)(base + A.lay.posbits);
-    S.mark = (int32_t *)(base + A.lay.mark);
+template <typename T>
+__device__ __forceinline__ void run_batch(const DpllArgs &A, const LdsT<T> &S) {
     span_begin(A.work_counter);
     for (;;) {
         uint32_t b = 0;
         if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
         b = uniform_u32(b);
         if (b >= (uint32_t)A.num_instances) break;
-        solve_instance(A, S, (int)b);
+        solve_instance<T>(A, S, (int)b);
         wave_sync();
     }
     span_end(A.work_counter);
+}
+
+// Narrow: each wave's image in its slice of the workgroup's LDS.
+__global__ void __launch_bounds__(256) dpll_batch_kernel(DpllArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = threadIdx.x >> 6;
+    run_batch<Narrow>(A, bind_storage<Narrow>(smem + (size_t)wave * A.lay.bytes, A.lay));
+}
+
+// Wide: one-wave workgroups, each wave's image in its own HBM arena of
+// A.lay.bytes (the flattened-apply scratch row stays in LDS).
+__global__ void __launch_bounds__(64) dpll_wide_kernel(DpllArgs A, unsigned char *arena) {
+    __shared__ __attribute__((aligned(16))) int32_t mark_s[64];
+    LdsT<Wide> S = bind_storage<Wide>(arena + (size_t)blockIdx.x * (size_t)A.lay.bytes, A.lay);
+    S.mark = mark_s;
+    run_batch<Wide>(A, S);
 }
 
 // ------------------------------------------------------------------ host side
@@ -874,6 +946,54 @@ static bool make_layout(int max_vars, int max_clauses, int max_lits, DpllLayout 
     return o <= 160u * 1024u;
 }
 
+// Wide storage (HBM arena per wave): 32-bit codes / indices / positions, 64-bit
+// clause and count words.  False when an offset would pass 4 GiB.
+static bool make_wide_layout(int max_vars, int max_clauses, int max_lits, DpllLayout *lay) {
+    if (max_vars < 0 || max_clauses < 0 || max_lits < 0) return false;
+    if (max_vars > (1 << 30) - 2 || max_clauses > (1 << 28) || max_lits > (1 << 30)) return false;
+    const uint64_t N = (uint64_t)max_vars + 1, M = (uint64_t)max_clauses + 1, Lc = (uint64_t)max_lits + 1;
+    auto a16 = [](uint64_t x) { return (x + 15u) & ~(uint64_t)15u; };
+    uint64_t o = 0;
+    uint64_t off[15];
+    off[0] = o;  o = a16(o + 4 * (Lc + 4));        // lit (+4: clause_counts reads in groups of four)
+    off[1] = o;  o = a16(o + 4 * M);               // coff
+    off[2] = o;  o = a16(o + 4 * (2 * N + 1));     // occoff
+    off[3] = o;  o = a16(o + 4 * Lc);              // occ
+    off[4] = o;  o = a16(o + 8 * M);               // cst
+    off[5] = o;  o = a16(o + 4 * N);               // vst
+    off[6] = o;  o = a16(o + 8 * N);               // cnt
+    off[7] = o;  o = a16(o + 8 * N);               // claim
+    off[8] = o;  o = a16(o + 4 * N);               // trail
+    off[9] = o;  o = a16(o + 4 * N);               // fvar
+    off[10] = o; o = a16(o + 4 * N);               // ftrail
+    off[11] = o; o = a16(o + 4 * M);               // units
+    off[12] = o; o = a16(o + 8 * ((M + 63) / 64)); // ubits
+    off[13] = o; o = a16(o + 8 * ((Lc + 63) / 64));// posbits
+    off[14] = o; o = a16(o + 4 * 64);              // mark (unused: LDS row)
+    o = (o + 255u) & ~(uint64_t)255u;              // arenas start on 256-B boundaries
+    if (o >= (1ull << 32)) return false;
+    lay->lit = (uint32_t)off[0];
+    lay->coff = (uint32_t)off[1];
+    lay->occoff = (uint32_t)off[2];
+    lay->occ = (uint32_t)off[3];
+    lay->cst = (uint32_t)off[4];
+    lay->vst = (uint32_t)off[5];
+    lay->cnt = (uint32_t)off[6];
+    lay->claim = (uint32_t)off[7];
+    lay->trail = (uint32_t)off[8];
+    lay->fvar = (uint32_t)off[9];
+    lay->ftrail = (uint32_t)off[10];
+    lay->units = (uint32_t)off[11];
+    lay->ubits = (uint32_t)off[12];
+    lay->posbits = (uint32_t)off[13];
+    lay->mark = (uint32_t)off[14];
+    lay->bytes = (uint32_t)o;
+    lay->lcap = max_lits;
+    lay->mcap = max_clauses;
+    lay->ncap = max_vars;
+    return true;
+}
+
 // Per-device launch state.  Each stream gets its own work counter, so batches
 // launched on different streams (a pipelined caller overlapping one batch's
 // tail with the next batch) never share a queue; launches on one stream are
@@ -886,6 +1006,8 @@ struct DeviceWork {
     // shrunk) and the stream's launch tag for the slot states
     std::unordered_map<hipStream_t, std::pair<void *, size_t>> split;
     std::unordered_map<hipStream_t, uint32_t> split_epoch;
+    // wide general kernel: per-wave HBM arenas per stream (grown, never shrunk)
+    std::unordered_map<hipStream_t, std::pair<void *, size_t>> arena;
     double ticks_per_s = 1e8;
     bool init = false;
 };
@@ -967,6 +1089,28 @@ static uint16_t *occ_scratch(hipStream_t stream, size_t bytes) {
     return slot.first;
 }
 
+// Per-wave arenas of the wide general kernel on `stream` (same lifetime rule).
+static void *arena_scratch(hipStream_t stream, size_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_work_mu);
+    if ((int)g_work.size() <= dev) g_work.resize(dev + 1);
+    auto &slot = g_work[dev].arena[stream];
+    if (slot.second >= bytes) return slot.first;
+    if (slot.first) {
+        if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+        (void)hipFree(slot.first);
+        slot = {nullptr, 0};
+    }
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        set_error("wide DPLL arenas: hipMalloc failed");
+        return nullptr;
+    }
+    slot = {p, bytes};
+    return slot.first;
+}
+
 // Branch-splitting scratch on `stream` (same lifetime rule as occ_scratch) and
 // the next launch tag of its slot states.
 static void *split_scratch(hipStream_t stream, size_t bytes, uint32_t *epoch) {
@@ -1004,7 +1148,7 @@ extern "C" int satmi_dpll_set_split(int enable) {
 
 extern "C" int satmi_dpll_set_kernel(int policy) {
     if (policy != SATMI_KERNEL_AUTO && policy != SATMI_KERNEL_GENERAL && policy != SATMI_KERNEL_SCAN &&
-        policy != SATMI_KERNEL_INC) {
+        policy != SATMI_KERNEL_INC && policy != SATMI_KERNEL_WIDE) {
         set_error("satmi_dpll_set_kernel: unknown policy");
         return SATMI_ERR_ARG;
     }
@@ -1035,9 +1179,15 @@ extern "C" int satmi_dpll_plan(int max_vars, int max_clauses, int max_lits, int 
         return rc;
     }
     DpllLayout lay;
-    if (!make_layout(max_vars, max_clauses, max_lits, &lay)) {
-        set_error("satmi_dpll_plan: instance too large for the LDS layout");
-        return SATMI_ERR_TOO_LARGE;
+    if (policy == SATMI_KERNEL_WIDE || !make_layout(max_vars, max_clauses, max_lits, &lay)) {
+        if (!make_wide_layout(max_vars, max_clauses, max_lits, &lay)) {
+            set_error("satmi_dpll_plan: instance too large for the wide (HBM arena) layout");
+            return SATMI_ERR_TOO_LARGE;
+        }
+        *kernel = SATMI_KERNEL_WIDE;
+        *lds_bytes_per_wave = 256;   // the arena is in HBM; LDS holds one scratch row
+        *waves_per_cu = 32;
+        return SATMI_OK;
     }
     *kernel = SATMI_KERNEL_GENERAL;
     *lds_bytes_per_wave = lay.bytes;
@@ -1139,15 +1289,58 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         return dpll_scan_launch(Lc);
     }
     DpllLayout lay;
-    if (!make_layout(max_vars, max_clauses, max_lits, &lay)) {
-        set_error("satmi_dpll_batch_device: instance too large for the LDS layout (vars <= 32767, "
-                  "clauses <= 65534, literals <= 65535, <= 160 KiB per wave)");
+    const bool wide = policy == SATMI_KERNEL_WIDE || !make_layout(max_vars, max_clauses, max_lits, &lay);
+    if (wide && !make_wide_layout(max_vars, max_clauses, max_lits, &lay)) {
+        set_error("satmi_dpll_batch_device: instance too large (wide layout: vars < 2^30, clauses <= 2^28, "
+                  "literals <= 2^30, < 4 GiB per wave)");
         return SATMI_ERR_TOO_LARGE;
     }
     DeviceWork *w = nullptr;
     uint32_t *wc = nullptr;
     int rc = device_work((hipStream_t)stream, &w, &wc);
     if (rc) return rc;
+    if (wide) {
+        // one-wave workgroups, each with an HBM arena; resident waves bounded by
+        // 32 per CU and by half the free device memory
+        int dev = 0, cus = 256;
+        SATMI_HIP(hipGetDevice(&dev));
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        size_t free_b = 0, total_b = 0;
+        SATMI_HIP(hipMemGetInfo(&free_b, &total_b));
+        const size_t per = lay.bytes;
+        const size_t by_mem = std::max<size_t>(1, (free_b / 2) / per);
+        const int grid = (int)std::min<size_t>({(size_t)num_instances, (size_t)cus * 32, by_mem});
+        unsigned char *arena = (unsigned char *)arena_scratch((hipStream_t)stream, (size_t)grid * per);
+        if (!arena) return SATMI_ERR_NOMEM;
+        DpllArgs A;
+        A.inst_clause_begin = d_inst_clause_begin;
+        A.clause_lit_begin = d_clause_lit_begin;
+        A.lits = d_lits;
+        A.inst_nvars = d_inst_nvars;
+        A.init_begin = d_init_begin;
+        A.init_lits = d_init_lits;
+        A.num_instances = num_instances;
+        A.mode = mode;
+        A.sol_cap = sol_cap;
+        A.sol_stride = sol_stride;
+        A.max_solutions = max_solutions;
+        A.node_limit = node_limit;
+        A.time_limit_ticks = time_limit_s > 0 ? (uint64_t)(time_limit_s * w->ticks_per_s) : 0;
+        A.status = d_status;
+        A.counters = d_counters;
+        A.sol_len = d_sol_len;
+        A.sol_lits = d_sol_lits;
+        A.root_len = d_root_len;
+        A.root_lits = d_root_lits;
+        A.work_counter = wc;
+        A.lay = lay;
+        hipStream_t s = (hipStream_t)stream;
+        SATMI_HIP(hipMemsetAsync(wc, 0, 24, s));   // counter + launch span (common.h)
+        hipLaunchKernelGGL(dpll_wide_kernel, dim3(grid), dim3(64), 0, s, A, arena);
+        SATMI_HIP(hipGetLastError());
+        return SATMI_OK;
+    }
     // Occupancy is set by LDS: pick the workgroup shape that keeps the most
     // waves resident (<= 32 waves and, conservatively, <= 16 workgroups per CU).
     int waves_per_wg = 1, wg_per_cu = 1, best_waves = 0;

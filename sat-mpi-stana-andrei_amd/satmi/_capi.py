@@ -20,7 +20,7 @@ COUNTER_NAMES = ("nodes", "decisions", "unit_props", "pure_assigns", "conflicts"
 DPLL_EXHAUSTED, DPLL_STOPPED, DPLL_NODE_LIMIT, DPLL_TIMEOUT, DPLL_TOO_LARGE = range(5)
 STATUS_NAMES = {0: "exhausted", 1: "stopped", 2: "node_limit", 3: "timeout", 4: "too_large"}
 RES_SAT, RES_UNSAT, RES_LIMIT = 1, 0, -1
-KERNEL_AUTO, KERNEL_GENERAL, KERNEL_SCAN, KERNEL_INC = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_GENERAL, KERNEL_SCAN, KERNEL_INC, KERNEL_WIDE = 0, 1, 2, 3, 4
 
 # exported symbols, checked by tests/test_capi_symbols.py against include/satmi.h
 EXPORTED = (

@@ -404,3 +404,75 @@ def test_branch_splitting_repeated_launches_one_stream():
         rs = _run_split(batch, True, max_solutions=1, sol_cap=1)
         assert (rs.counters[:, :7] == ru.counters[:, :7]).all()
         assert (rs.sol_lits == ru.sol_lits).all()
+
+
+@pytest.mark.parametrize("seed,nmax,kmax,mmax", [(11, 12, 4, 60), (12, 400, 300, 30)])
+def test_wide_kernel_matches_general_and_oracle(seed, nmax, kmax, mmax):
+    """The general kernel's wide form (per-wave HBM arena, 32-bit indices,
+    SATMI_KERNEL_WIDE) against its LDS form and the oracle, REF and SOUND
+    modes, first model and full enumeration: every counter, every solution,
+    the root assignment.  kmax=300 reaches clauses past the LDS form's
+    255-literal limit (there only the oracle is the reference)."""
+    fs = _random_mix(seed, 160, nmax, kmax, mmax)
+    long_clause = any(len(c) > 255 for f in fs for c in f)
+    for mode, maxs, cap in (("ref", 0, 32), ("sound", 1, 1), ("sound", 0, 32)):
+        _capi.set_kernel(_capi.KERNEL_WIDE)
+        try:
+            rw = dpll_batch(fs, mode=mode, max_solutions=maxs, sol_cap=cap, node_limit=3000)
+        finally:
+            _capi.set_kernel(_capi.KERNEL_AUTO)
+        if not long_clause:
+            _capi.set_kernel(_capi.KERNEL_GENERAL)
+            try:
+                rg = dpll_batch(fs, mode=mode, max_solutions=maxs, sol_cap=cap, node_limit=3000)
+            finally:
+                _capi.set_kernel(_capi.KERNEL_AUTO)
+            assert (rw.status == rg.status).all()
+            assert (rw.counters[:, :7] == rg.counters[:, :7]).all()
+            assert (rw.root_len == rg.root_len).all()
+        for b in range(0, len(fs), 1 if long_clause else 5):
+            o = oracle.dpll(fs[b], mode, max_solutions=maxs, node_limit=3000, sol_cap=cap)
+            assert int(rw.status[b]) == o["status"], (mode, b)
+            for key in CTR:
+                assert rw.counter_dict(b)[key] == o["counters"][key], (mode, key, b)
+            assert rw.solutions(b) == o["solutions"][:cap], (mode, b)
+            assert rw.root_assignment(b) == o["root_assign"]
+
+
+def test_wide_kernel_reference_golden(golden_dir):
+    cases = _golden(golden_dir, "dpll_ref.json")
+    cap = max(len(c["solutions"]) for c in cases) + 1
+    _capi.set_kernel(_capi.KERNEL_WIDE)
+    try:
+        r = dpll_batch([c["formula"] for c in cases], mode="ref", max_solutions=0, sol_cap=cap,
+                       inits=[c["init"] for c in cases], time_limit=20.0)
+    finally:
+        _capi.set_kernel(_capi.KERNEL_AUTO)
+    for b, c in enumerate(cases):
+        assert r.solutions(b) == c["solutions"]
+        got = r.counter_dict(b)
+        for k, v in c["counters"].items():
+            assert got[k] == v, (k, c["formula"])
+
+
+@pytest.mark.parametrize("clauses,max_len,nvars,cap", [(1000, 100, 100, 40), (5000, 1000, 1000, 4)])
+def test_reference_menu_shapes_run_wide(clauses, max_len, nvars, cap):
+    """The reference's own menu runs beyond one wave's LDS image: rezultat.txt:248-250
+    (1000 clauses, avg length ~50, 100 variables) and :488-490 (5000 clauses, avg
+    length ~500, 1000 variables), drawn with REF.py:21-29's generator.  AUTO
+    dispatch takes the wide kernel; node-capped REF and SOUND searches equal the
+    oracle (status, counters, solutions)."""
+    from satmi.solvers import generate_large_formula
+    random.seed(clauses + nvars)
+    f = generate_large_formula(clauses, max_len, nvars)
+    L = sum(len(c) for c in f)
+    kern, _, _ = _capi.plan(nvars, clauses, L, max(len(c) for c in f), mode=_capi.MODE_REF)
+    assert kern == _capi.KERNEL_WIDE
+    for mode, maxs in (("ref", 0), ("sound", 1)):
+        r = dpll_batch([f], mode=mode, max_solutions=maxs, node_limit=cap, sol_cap=4)
+        o = oracle.dpll(f, mode, max_solutions=maxs, node_limit=cap, sol_cap=4)
+        assert int(r.status[0]) == o["status"]
+        for key in CTR:
+            assert r.counter_dict(0)[key] == o["counters"][key], (mode, key)
+        assert r.solutions(0) == o["solutions"][:4]
+        assert r.root_assignment(0) == o["root_assign"]

@@ -28,3 +28,21 @@ def test_menu_session_on_gpu_solvers(tmp_path):
     want = f"Found {nsol} solution(s)" if nsol else "No solutions found"
     assert want in rows["DPLL"] and want in rows["Hybrid"]
     assert "- Clauses: 5" in text and "- Variables: 4" in text
+
+
+def test_menu_large_formula_times_out_like_reference():
+    """rezultat.txt:248-262: on the 1000-clause menu formula (avg length ~50,
+    100 variables) the reference's DPLL and Hybrid rows read "Timeout after 60
+    seconds".  The GPU drop-in runs the same enumeration (wide kernel: the
+    image exceeds one wave's LDS) and reports the same timeout row, here with a
+    2-second deadline."""
+    import random
+
+    from satmi.solvers import dpll_optimized, generate_large_formula, hybrid_solver
+    random.seed(1100)
+    f = generate_large_formula(1000, 100, 100)
+    results = driver.run_solvers(f, [("DPLL", dpll_optimized), ("Hybrid", hybrid_solver)], timeout=2,
+                                 print_fn=lambda *a: None)
+    for name in ("DPLL", "Hybrid"):
+        assert results[name]["output"] == "Timeout after 2 seconds", results[name]
+        assert results[name]["time"] == 2
