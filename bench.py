@@ -48,6 +48,7 @@ from satmi.shard import shard_range  # noqa: E402
 
 METRIC = "instances solved/sec, random 3-SAT n=100 α=4.26; unit-props/sec; HBM GB/s"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SHADER_CLOCK_HZ = 2.4e9        # MI355X_MICROARCH.md: peak engine clock (the LDS-issue peak of dp_roofline)
 KERNELS = {_capi.KERNEL_SCAN: "dpll_scan_kernel", _capi.KERNEL_INC: "dpll_scan_kernel (incremental rounds)",
            _capi.KERNEL_GENERAL: "dpll_batch_kernel"}
 
@@ -81,6 +82,7 @@ def parse():
     p.add_argument("--kernel", choices=("auto", "inc", "scan", "general"), default="auto",
                    help="DPLL kernel policy (satmi_dpll_set_kernel); auto = incremental clause kernel")
     p.add_argument("--no-split", action="store_true", help="disable branch splitting (satmi_dpll_set_split)")
+    p.add_argument("--helpers-per-cu", type=int, default=0, help="branch-splitting helpers per CU (0 = library default)")
     p.add_argument("--streams", type=int, default=2, choices=(1, 2, 3, 4),
                    help="HIP streams (each with its own resident batch) the steps rotate over")
     a = p.parse_args()
@@ -190,6 +192,28 @@ def issue_roofline(preset, per_gpu, kernel_ms):
             "clock_hz": e["effective_clock_hz"], "source": e["source"], "stale": e["kernel_src_sha256_16"] != sha}
 
 
+def dp_roofline(stats, cus, clock_hz):
+    """Davis-Putnam (php-dp): the subsumption filter dominates (dp_subsume_tiled_kernel,
+    one lane per new clause, candidate keys broadcast from LDS).  Its binding
+    resource is the LDS issue pipe: one ds_read of a K-word key serves the 256
+    lanes of a workgroup, so a CU retires at most 64 / K subset tests per
+    cycle (64 lanes x one key word per LDS instruction per cycle).  achieved =
+    subset tests performed / the filter's device time (HIP events)."""
+    if not stats:
+        return None
+    tests = sum(s["subset_tests"] for s in stats) / len(stats)
+    ms = sum(s["subsume_ms"] for s in stats) / len(stats)
+    K = stats[-1]["words"]
+    if ms <= 0 or K <= 0:
+        return None
+    ach = tests / (ms * 1e-3)
+    peak = cus * clock_hz * 64.0 / K
+    return {"bound": "lds-issue", "achieved": ach, "peak": peak, "unit": "subset-tests/s", "frac": ach / peak,
+            "traffic": None, "kernel": "dp_subsume_tiled_kernel", "kernel_ms_per_step": ms,
+            "subset_tests_per_step": tests, "new_clauses_per_step": sum(s["new_clauses"] for s in stats) / len(stats),
+            "key_words": K, "clock_hz": clock_hz}
+
+
 def saturation_roofline(workload, stats, last):
     """Resolution (php-res): the dominant of its two kernels per step, timed by
     HIP events on the library's stream (satmi_resolution_last_stats).  Claim
@@ -220,6 +244,7 @@ def saturation_main(args):
     verdict out: the boundary these solvers have, REF.py:63-130).  Each rank
     solves its own replica (one formula does not shard)."""
     from satmi.dp import eliminate
+    from satmi.dp import last_stats as dp_stats
     from satmi.resolution import last_stats as res_stats
     from satmi.resolution import resolve
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -251,8 +276,7 @@ def saturation_main(args):
     for _ in range(args.steps):
         last = run()
         done += work(last)
-        if args.workload == "php-res":
-            stats.append(res_stats())
+        stats.append(res_stats() if args.workload == "php-res" else dp_stats())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -267,7 +291,9 @@ def saturation_main(args):
            "config": {"workload": metric_desc + " (BASELINE configs[3]); replicas across ranks",
                       "preset": args.workload, "parallelism": f"replicas x{world}"},
            "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
-           "roofline": saturation_roofline(args.workload, stats, last)}
+           "roofline": saturation_roofline(args.workload, stats, last) if args.workload == "php-res" else
+           dp_roofline(stats, torch.cuda.get_device_properties(local).multi_processor_count,
+                       SHADER_CLOCK_HZ)}
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.profile_steps:
@@ -302,7 +328,7 @@ def main():
     L = _capi.load()
     _capi.set_kernel({"auto": _capi.KERNEL_AUTO, "inc": _capi.KERNEL_INC, "scan": _capi.KERNEL_SCAN,
                       "general": _capi.KERNEL_GENERAL}[args.kernel])
-    _capi.set_split(not args.no_split)
+    _capi.set_split(not args.no_split, args.helpers_per_cu)
     NS = args.streams
 
     n, k = args.n, args.k
@@ -460,6 +486,8 @@ def main():
         "roofline": roof,
         "roofline_issue": issue_roofline(args.workload, B, kernel_ms),
     }
+    if not args.no_split:   # the last launch's branch-splitting statistics (satmi_dpll_split_stats)
+        out["branch_split"] = _capi.split_stats(streams[(args.steps - 1) % NS].cuda_stream)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and not args.profile_steps:
             host = cnf.CnfBatch(icb.cpu().numpy(), clb.cpu().numpy(), lits.cpu().numpy(), nv.cpu().numpy())

@@ -158,6 +158,13 @@ int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_li
                   int trace_cap, int32_t *h_steps, int32_t *h_rec_lits, int64_t rec_lit_cap,
                   int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_step_off, int rec_step_cap);
 
+/* Work of the last satmi_dp_host call's subsumption filter (REF.py:122-125):
+ * elimination steps, subset tests performed, new (non-tautological) clauses
+ * filtered, bytes of candidate keys, key words per clause, and the filter's
+ * device time (HIP events on its stream), for rooflines. */
+int satmi_dp_last_stats(int64_t *steps, int64_t *subset_tests, int64_t *new_clauses, int64_t *candidate_bytes,
+                        int *words, double *subsume_ms);
+
 /* Device-side span of the last DPLL launch on `stream`: enqueues (on that
  * stream, after the launch) a copy of two uint64 s_memrealtime ticks into
  * d_span: [0] = ~(first wave's start), [1] = last wave's end, so the launch
@@ -197,8 +204,17 @@ int satmi_dpll_set_kernel(int policy);
  * backtracking reaches the branch.  Statuses, counters and models are those of
  * the unsplit search (branches a sequential search would not have visited are
  * cancelled and count nothing).  Applies to SOUND-mode launches with
- * max_solutions == 1, no node limit and no time limit. */
-int satmi_dpll_set_split(int enable);
+ * max_solutions == 1, no node limit and no time limit.
+ *   helpers_per_cu  wavefronts per CU that stay as helpers once the queue
+ *                   drains (0 = default 4); the others exit, freeing their CU
+ *                   slots for a launch queued on another stream */
+int satmi_dpll_set_split(int enable, int helpers_per_cu);
+
+/* Branch-splitting statistics of the last split launch on `stream` (waits for
+ * the stream): out[0..6] = donations, helper tickets, subtrees run by helpers,
+ * donations taken back by their donors, waves that registered as helpers,
+ * donors' ticks spent waiting on helpers, root instances finished. */
+int satmi_dpll_split_stats(void *stream, int64_t *out);
 
 /* The launch satmi_dpll_batch_device would make for this batch shape under the
  * current policy: *kernel = SATMI_KERNEL_SCAN or SATMI_KERNEL_GENERAL, LDS

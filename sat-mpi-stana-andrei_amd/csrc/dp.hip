@@ -244,6 +244,68 @@ __global__ void __launch_bounds__(256) dp_subsume_kernel(ClauseList L, const int
     }
 }
 
+// The same filter for K <= 8 words per clause (<= 256 variables), one LANE per
+// new clause with its key in registers: a workgroup stages 256 candidate
+// subsets at a time in LDS (remaining clauses, then earlier new clauses) and
+// every lane tests its clause against each staged key -- all lanes read the same
+// LDS address (a broadcast, no bank conflicts), so one key load serves 256
+// tests and the candidate lists are read once per workgroup instead of once
+// per new clause.  The workgroup stops when all its lanes found a subset.
+// tests_out: subset tests performed (roofline input).
+constexpr int SUB_TILE = 256;
+template <int K>
+__global__ void __launch_bounds__(SUB_TILE) dp_subsume_tiled_kernel(ClauseList L, const int64_t *rlist, int64_t nrem,
+                                                                    const uint64_t *rbits, const int64_t *ntlist,
+                                                                    int64_t m, int64_t *kept,
+                                                                    unsigned long long *tests_out) {
+    __shared__ uint64_t tile[SUB_TILE][K];
+    const int tid = threadIdx.x;
+    const int64_t k = (int64_t)blockIdx.x * SUB_TILE + tid;
+    const bool valid = k < m;
+    uint64_t x[K];
+#pragma unroll
+    for (int w = 0; w < K; ++w) x[w] = valid ? rbits[ntlist[k] * K + w] : 0ull;
+    bool alive = valid;
+    uint64_t tests = 0;
+    const int64_t kmax = min(m, (int64_t)(blockIdx.x + 1) * SUB_TILE) - 1;   // the block's last new clause
+    // pass 0: remaining clauses (all of them); pass 1: new clauses before k
+    for (int pass = 0; pass < 2; ++pass) {
+        const int64_t n = pass == 0 ? nrem : kmax;
+        for (int64_t e0 = 0; e0 < n; e0 += SUB_TILE) {
+            if (!__syncthreads_or(alive)) break;
+            const int64_t e = e0 + tid;
+            if (e < n) {
+                const uint64_t *src = pass == 0 ? L.bits + rlist[e] * K : rbits + ntlist[e] * K;
+#pragma unroll
+                for (int w = 0; w < K; ++w) tile[tid][w] = src[w];
+            }
+            __syncthreads();
+            const int cnt = (int)min((int64_t)SUB_TILE, (pass == 0 ? n : k) - e0);
+            if (alive) {
+                for (int j = 0; j < cnt; ++j) {
+                    uint64_t out = 0;
+#pragma unroll
+                    for (int w = 0; w < K; ++w) out |= tile[j][w] & ~x[w];
+                    ++tests;
+                    if (out == 0ull) {
+                        alive = false;
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (valid) kept[k] = alive;
+    // one atomic per workgroup
+    __shared__ unsigned long long tsum;
+    if (tid == 0) tsum = 0;
+    __syncthreads();
+    atomicAdd(&tsum, (unsigned long long)tests);
+    __syncthreads();
+    if (tid == 0) atomicAdd(tests_out, tsum);
+}
+
 // kept resolvent images: (pc - {var}) | (nc - {-var})  (REF.py:114)
 __global__ void dp_build_kernel(Images A, Images B, const int64_t *ntlist, const int64_t *kflag, const int64_t *kpos,
                                 int64_t m, int64_t nn, Images R, int *overflow) {
@@ -371,6 +433,15 @@ struct Img {
     }
 };
 
+// Work and device time of the last satmi_dp_host call's subsumption filter
+// (HIP events on its stream), for bench.py's roofline.
+struct DpStats {
+    int64_t steps = 0, tests = 0, new_clauses = 0, candidates_bytes = 0;
+    double subsume_ms = 0.0;
+    int words = 0;
+};
+DpStats g_dp_stats;
+
 // ordered compaction of flag[n] into out (indices); returns the count
 int compact(const int64_t *flag, int64_t n, Buf &pos, Buf &tiles, Buf &grand, Buf &out, int64_t *count,
             hipStream_t s) {
@@ -459,6 +530,19 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             SATMI_HIP(hipGetLastError());
         }
     }
+    // subsumption-filter timing (satmi_dp_last_stats); misc[40..48) counts its subset tests
+    struct Ev {
+        hipEvent_t e[2] = {nullptr, nullptr};
+        ~Ev() {
+            for (auto x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } evs;
+    SATMI_HIP(hipEventCreate(&evs.e[0]));
+    SATMI_HIP(hipEventCreate(&evs.e[1]));
+    hipEvent_t *ev_sub = evs.e;
+    g_dp_stats = DpStats{};
+    g_dp_stats.words = K;
     DP_TRY(firstpos.need(8 * (size_t)std::max(V, 1)));
     DP_TRY(order.need(4 * (size_t)std::max(V, 1)));
     const int64_t popcap = cap_for(V);
@@ -557,10 +641,30 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         int64_t nkept = 0;
         if (m > 0) {
             DP_TRY(kept.need(8 * (size_t)m));
-            hipLaunchKernelGGL(dp_subsume_kernel, dim3(grid_for(m * 64)), dim3(PRIM_BLOCK), 0, s, Lc,
-                               rlist.as<int64_t>(), nr, rbits.as<uint64_t>(), ntlist.as<int64_t>(), m, K,
-                               kept.as<int64_t>());
+            const int nb = (int)((m + SUB_TILE - 1) / SUB_TILE);
+            const int64_t *rl = rlist.as<int64_t>(), *ntl = ntlist.as<int64_t>();
+            const uint64_t *rb = rbits.as<uint64_t>();
+            int64_t *kp = kept.as<int64_t>();
+            unsigned long long *tc = (unsigned long long *)(misc.as<char>() + 40);
+            SATMI_HIP(hipEventRecord(ev_sub[0], s));
+            if (K == 2)
+                hipLaunchKernelGGL((dp_subsume_tiled_kernel<2>), dim3(nb), dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl, m, kp, tc);
+            else if (K == 4)
+                hipLaunchKernelGGL((dp_subsume_tiled_kernel<4>), dim3(nb), dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl, m, kp, tc);
+            else if (K == 6)
+                hipLaunchKernelGGL((dp_subsume_tiled_kernel<6>), dim3(nb), dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl, m, kp, tc);
+            else if (K == 8)
+                hipLaunchKernelGGL((dp_subsume_tiled_kernel<8>), dim3(nb), dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl, m, kp, tc);
+            else
+                hipLaunchKernelGGL(dp_subsume_kernel, dim3(grid_for(m * 64)), dim3(PRIM_BLOCK), 0, s, Lc, rl, nr, rb,
+                                   ntl, m, K, kp);
+            SATMI_HIP(hipEventRecord(ev_sub[1], s));
             SATMI_HIP(hipGetLastError());
+            SATMI_HIP(hipEventSynchronize(ev_sub[1]));
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, ev_sub[0], ev_sub[1]) == hipSuccess) g_dp_stats.subsume_ms += ms;
+            g_dp_stats.new_clauses += m;
+            g_dp_stats.candidates_bytes += (nr + m) * K * 8;
             DP_TRY(compact(kept.as<int64_t>(), m, kpos, tiles, grand, klist, &nkept, s));
         }
         if (nkept > 0) {
@@ -636,7 +740,24 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         }
     }
     SATMI_HIP(hipStreamSynchronize(s));
+    {
+        unsigned long long tests = 0;
+        SATMI_HIP(hipMemcpy(&tests, misc.as<char>() + 40, 8, hipMemcpyDeviceToHost));
+        g_dp_stats.tests = (int64_t)tests;
+        g_dp_stats.steps = steps;
+    }
     *h_result = result;
     *h_steps = steps;
+    return SATMI_OK;
+}
+
+extern "C" int satmi_dp_last_stats(int64_t *steps, int64_t *subset_tests, int64_t *new_clauses,
+                                   int64_t *candidate_bytes, int *words, double *subsume_ms) {
+    if (steps) *steps = g_dp_stats.steps;
+    if (subset_tests) *subset_tests = g_dp_stats.tests;
+    if (new_clauses) *new_clauses = g_dp_stats.new_clauses;
+    if (candidate_bytes) *candidate_bytes = g_dp_stats.candidates_bytes;
+    if (words) *words = g_dp_stats.words;
+    if (subsume_ms) *subsume_ms = g_dp_stats.subsume_ms;
     return SATMI_OK;
 }

@@ -1015,6 +1015,7 @@ static std::mutex g_work_mu;
 static std::vector<DeviceWork> g_work;
 static std::atomic<int> g_kernel_policy{SATMI_KERNEL_AUTO};
 static std::atomic<int> g_split_enable{1};
+static std::atomic<int> g_split_helpers{SPLIT_HELPERS_PER_CU};
 
 static int device_work(hipStream_t stream, DeviceWork **out, uint32_t **counter) {
     int dev = 0;
@@ -1141,8 +1142,37 @@ static void *split_scratch(hipStream_t stream, size_t bytes, uint32_t *epoch) {
     return slot.first;
 }
 
-extern "C" int satmi_dpll_set_split(int enable) {
+extern "C" int satmi_dpll_split_stats(void *stream, int64_t *out) {
+    if (!out) {
+        set_error("satmi_dpll_split_stats: out is NULL");
+        return SATMI_ERR_ARG;
+    }
+    for (int i = 0; i < 7; ++i) out[i] = 0;
+    int dev = 0;
+    SATMI_HIP(hipGetDevice(&dev));
+    void *head = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_work_mu);
+        if ((int)g_work.size() > dev) {
+            auto it = g_work[dev].split.find((hipStream_t)stream);
+            if (it != g_work[dev].split.end()) head = it->second.first;
+        }
+    }
+    if (!head) return SATMI_OK;   // no split launch on this stream yet
+    unsigned char h[SPLIT_HEAD_BYTES];
+    SATMI_HIP(hipStreamSynchronize((hipStream_t)stream));
+    SATMI_HIP(hipMemcpy(h, head, sizeof(h), hipMemcpyDeviceToHost));
+    dpll_split_decode(h, out);
+    return SATMI_OK;
+}
+
+extern "C" int satmi_dpll_set_split(int enable, int helpers_per_cu) {
+    if (helpers_per_cu < 0 || helpers_per_cu > 32) {
+        set_error("satmi_dpll_set_split: helpers_per_cu must be in [0, 32]");
+        return SATMI_ERR_ARG;
+    }
     g_split_enable.store(enable ? 1 : 0);
+    g_split_helpers.store(helpers_per_cu ? helpers_per_cu : SPLIT_HELPERS_PER_CU);
     return SATMI_OK;
 }
 
@@ -1282,6 +1312,7 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         // branch splitting reproduces the sequential search exactly only when
         // the search stops at its first model and nothing else cuts it short
         Lc.split = g_split_enable.load() && max_solutions == 1 && node_limit <= 0 && time_limit_s <= 0;
+        Lc.split_helpers_per_cu = g_split_helpers.load();
         Lc.split_alloc = [stream](size_t bytes, uint32_t *epoch) {
             return split_scratch((hipStream_t)stream, bytes, epoch);
         };

@@ -8,6 +8,8 @@
 
 namespace satmi {
 
+constexpr int SPLIT_HELPERS_PER_CU = 4;
+
 struct ScanLaunch {
     int num_instances;
     const int32_t *inst_clause_begin, *clause_lit_begin, *lits, *inst_nvars;
@@ -30,6 +32,7 @@ struct ScanLaunch {
     // `stream` and the launch's tag for the slot states (distinct per launch on
     // the stream), nullptr on failure
     bool split = false;
+    int split_helpers_per_cu = SPLIT_HELPERS_PER_CU;   // waves per CU that stay as helpers once the queue drains
     std::function<void *(size_t, uint32_t *)> split_alloc;
 };
 
@@ -42,6 +45,11 @@ bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_cla
 // and the LDS bytes per wave of that launch (dynamic image + static literal states).
 int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, bool inc, int *waves_per_cu,
                        uint32_t *lds_per_wave = nullptr);
+
+// Bytes of the splitting scratch head, and its statistics decoded from a host
+// copy of it: [donations, tickets, claims, reclaims, helpers, wait_ticks, done].
+constexpr int SPLIT_HEAD_BYTES = 512;
+void dpll_split_decode(const void *head, int64_t out[7]);
 
 // Launch on L.stream (asynchronous).  The caller has checked eligibility and
 // zeroed *L.work_counter on the stream.

@@ -764,22 +764,29 @@ __device__ uint64_t flush_counters(int64_t *ctr, Ctr32 &c, bool &flushed) {
 // through (agent atomic stores), `s_waitcnt vmcnt(0)`, then the state flag by
 // an agent atomic; the reader polls the flag relaxed, then one agent acquire
 // and plain loads.  Flags and payload live on separate 128-B lines.
-struct SplitCtl {
-    uint32_t pub;      // slots allocated
-    uint32_t taken;    // slots ticketed by helpers
-    int32_t want;      // open requests of idle waves
-    uint32_t done;     // root instances finished
-};
-// Head of the splitting scratch, rewritten before each launch; the slot pool
-// follows at SPLIT_POOL_OFF, then the per-wave donation stacks.
+// Head of the splitting scratch, rewritten before each launch (the slot pool
+// follows at SPLIT_POOL_OFF, then the per-wave donation stacks).  One 128-B
+// line per access pattern: the queue line is polled by the helpers, the
+// request line read by every searching wave every SPLIT_MASK + 1 decisions --
+// kept apart so that polling never queues the searches' reads.
 struct SplitCfg {
-    SplitCtl ctl;              // zero at launch
-    uint32_t pad0[12];
-    int32_t slot_cap, slot_bytes, dstack_cap;
+    uint32_t pub;              // line 0: slots allocated
+    uint32_t taken;            //         slots ticketed by helpers
+    uint32_t pad0[30];
+    int32_t want;              // line 1: open requests of idle helpers
+    uint32_t pad1[31];
+    uint32_t done;             // line 2: root instances finished
+    int32_t helpers;           //         waves that registered as helpers
+    uint32_t claims, reclaims; //         statistics: subtrees run by helpers, taken back by donors
+    unsigned long long wait_ticks;   //   donors' time waiting on helpers
+    uint32_t pad2[26];
+    int32_t slot_cap, slot_bytes, dstack_cap;   // line 3: geometry (read only)
     uint32_t epoch;            // launch tag of the slot states (the pool is not cleared between launches)
-    uint32_t pad1[12];
+    int32_t max_helpers;       // waves beyond this count exit when the queue drains (their CU slots go
+                               // to the next launch on another stream)
+    uint32_t pad3[27];
 };
-constexpr int SPLIT_POOL_OFF = 128;
+constexpr int SPLIT_POOL_OFF = 512;
 static_assert(sizeof(SplitCfg) == SPLIT_POOL_OFF, "SplitCfg layout");
 constexpr uint32_t SPLIT_MASK = 15u;   // a donation check every 16 decisions
 enum : uint32_t { SL_PENDING = 1, SL_RUNNING = 2, SL_DONE = 3, SL_RECLAIMED = 4 };
@@ -846,9 +853,9 @@ __device__ void try_donate(const ScanArgs &A, const SLds<K, C> &S, int depth, in
     constexpr uint32_t PHASE = SLds<K, C>::PHASE_BIT, DON = SLds<K, C>::PHASE_BIT;
     const int ln = lane_id_here();
     int old = 0;
-    if (ln == 0) old = add_agent(&A.split->ctl.want, -1);
+    if (ln == 0) old = add_agent(&A.split->want, -1);
     if (uniform_i32(old) <= 0) {
-        if (ln == 0) add_agent(&A.split->ctl.want, 1);
+        if (ln == 0) add_agent(&A.split->want, 1);
         return;
     }
     int j = -1;
@@ -864,12 +871,12 @@ __device__ void try_donate(const ScanArgs &A, const SLds<K, C> &S, int depth, in
     int s = -1;
     if (j >= 0 && nd < A.split->dstack_cap) {
         uint32_t x = 0;
-        if (ln == 0) x = add_agent(&A.split->ctl.pub, 1u);
+        if (ln == 0) x = add_agent(&A.split->pub, 1u);
         x = uniform_u32(x);
         if (x < (uint32_t)A.split->slot_cap) s = (int)x;
     }
     if (s < 0) {
-        if (ln == 0) add_agent(&A.split->ctl.want, 1);
+        if (ln == 0) add_agent(&A.split->want, 1);
         return;
     }
     const SlotRef r = slot_ref(A, s);
@@ -911,7 +918,10 @@ __device__ int take_donation(const ScanArgs &A, int s, const SlotFlags *mine, in
     const SlotRef r = slot_ref(A, s);
     uint32_t prev = 0;
     if (lane_id_here() == 0) prev = cas_agent(&r.f->state, slot_state(A, SL_PENDING), slot_state(A, SL_RECLAIMED));
-    if (uniform_u32(prev) == slot_state(A, SL_PENDING)) return TAKE_LOCAL;
+    if (uniform_u32(prev) == slot_state(A, SL_PENDING)) {
+        if (lane_id_here() == 0) add_agent(&A.split->reclaims, 1u);
+        return TAKE_LOCAL;
+    }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (uniform_u32(ld_agent(&r.f->state)) == slot_state(A, SL_DONE)) break;
@@ -921,7 +931,11 @@ __device__ int take_donation(const ScanArgs &A, int s, const SlotFlags *mine, in
         }
         __builtin_amdgcn_s_sleep(8);
     }
-    if (lane_id_here() == 0) add_agent(&ctr[SATMI_CTR_TICKS], -(int64_t)(__builtin_amdgcn_s_memrealtime() - t0));
+    const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
+    if (lane_id_here() == 0) {
+        add_agent(&ctr[SATMI_CTR_TICKS], -(int64_t)dt);
+        add_agent(&A.split->wait_ticks, (unsigned long long)dt);
+    }
     acquire_agent();
     return uniform_i32(r.h->status) == SATMI_DPLL_STOPPED ? TAKE_SAT : TAKE_UNSAT;
 }
@@ -1093,7 +1107,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                         state = ST_DONE;
                         continue;
                     }
-                    if (uniform_i32(ld_agent(&A.split->ctl.want)) > 0) try_donate<K>(A, S, depth, b, dst, nd);
+                    if (uniform_i32(ld_agent(&A.split->want)) > 0) try_donate<K>(A, S, depth, b, dst, nd);
                 }
                 ep = next_decision_epoch<K>(S, n, ep);
                 if (ln == 0) {
@@ -1235,16 +1249,19 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
 // would otherwise be hoisted into registers held across the node loop.
 __device__ __forceinline__ int2 next_donation(SplitCfg *cfg, int num_instances) {
     const int ln = lane_id();
-    for (;;) {
-        if (uniform_u32(ld_agent(&cfg->ctl.done)) >= (uint32_t)num_instances) return make_int2(-1, -1);
-        const uint32_t t = uniform_u32(ld_agent(&cfg->ctl.taken));
-        const uint32_t p = min(uniform_u32(ld_agent(&cfg->ctl.pub)), (uint32_t)cfg->slot_cap);
+    for (uint32_t polls = 0;; ++polls) {
+        if ((polls & 7u) == 0u && uniform_u32(ld_agent(&cfg->done)) >= (uint32_t)num_instances)
+            return make_int2(-1, -1);
+        // pub and taken in one load: the queue line is the only one a helper polls
+        const unsigned long long q = ld_agent((unsigned long long *)&cfg->pub);
+        const uint32_t p = min(uniform_u32((uint32_t)q), (uint32_t)cfg->slot_cap);
+        const uint32_t t = uniform_u32((uint32_t)(q >> 32));
         if (t >= p) {
-            __builtin_amdgcn_s_sleep(32);
+            __builtin_amdgcn_s_sleep(127);   // ~8k cycles between polls
             continue;
         }
         uint32_t got = 0;
-        if (ln == 0) got = cas_agent(&cfg->ctl.taken, t, t + 1u);
+        if (ln == 0) got = cas_agent(&cfg->taken, t, t + 1u);
         if (uniform_u32(got) != t) continue;
         unsigned char *slot = (unsigned char *)cfg + SPLIT_POOL_OFF + (size_t)t * (size_t)cfg->slot_bytes;
         SlotFlags *f = (SlotFlags *)slot;
@@ -1254,9 +1271,10 @@ __device__ __forceinline__ int2 next_donation(SplitCfg *cfg, int num_instances) 
         uint32_t prev = 0;
         if (ln == 0) prev = cas_agent(&f->state, pending, (cfg->epoch << 4) | SL_RUNNING);
         if (uniform_u32(prev) != pending) {   // reclaimed by its donor
-            if (ln == 0) add_agent(&cfg->ctl.want, 1);
+            if (ln == 0) add_agent(&cfg->want, 1);
             continue;
         }
+        if (ln == 0) add_agent(&cfg->claims, 1u);
         acquire_agent();
         return make_int2(uniform_i32(((SlotHdr *)(slot + SLOT_HDR_OFF))->inst), (int)t);
     }
@@ -1279,8 +1297,12 @@ __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) 
                 b = (int)x;
             } else {
                 if (!A.split) break;
+                // a bounded set of helpers stays; the rest free their slots
+                int h = 0;
+                if (ln == 0) h = add_agent(&A.split->helpers, 1);
+                if (uniform_i32(h) >= A.split->max_helpers) break;
                 draining = true;
-                if (ln == 0) add_agent(&A.split->ctl.want, 1);
+                if (ln == 0) add_agent(&A.split->want, 1);
             }
         }
         if (draining) {
@@ -1291,7 +1313,7 @@ __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) 
         }
         // wave-uniform (a divergent-looking b costs 64-bit VGPR address math)
         solve_instance<K, INC, C>(A, S, uniform_i32(b), uniform_i32(task), dst);
-        if (A.split && ln == 0) add_agent(task < 0 ? (int32_t *)&A.split->ctl.done : &A.split->ctl.want, 1);
+        if (A.split && ln == 0) add_agent(task < 0 ? (int32_t *)&A.split->done : &A.split->want, 1);
         wave_sync();
     }
 }
@@ -1512,6 +1534,18 @@ void launch_kernel(int K, int lvs, dim3 g, dim3 blk, uint32_t wg_lds, hipStream_
 
 }  // namespace
 
+void dpll_split_decode(const void *head, int64_t out[7]) {
+    static_assert(SPLIT_HEAD_BYTES == SPLIT_POOL_OFF, "split head");
+    const SplitCfg *c = (const SplitCfg *)head;
+    out[0] = c->pub;
+    out[1] = c->taken;
+    out[2] = c->claims;
+    out[3] = c->reclaims;
+    out[4] = c->helpers;
+    out[5] = (int64_t)c->wait_ticks;
+    out[6] = c->done;
+}
+
 bool dpll_scan_eligible(int max_vars, int max_clauses, int max_lits, int max_clause_len, bool inc,
                         uint32_t *lds_bytes) {
     const int K = pick_k(max_vars, max_clause_len);
@@ -1580,6 +1614,7 @@ int dpll_scan_launch(const ScanLaunch &L) {
         cfg.slot_bytes = slot_bytes_for(ncap, cbytes);
         cfg.slot_cap = (int)std::min<size_t>(1u << 18, ((size_t)256 << 20) / (size_t)cfg.slot_bytes);
         cfg.dstack_cap = ncap + 1;
+        cfg.max_helpers = L.num_cus * L.split_helpers_per_cu;
         const size_t pool = (size_t)cfg.slot_cap * (size_t)cfg.slot_bytes;
         const size_t stacks = (size_t)grid * (size_t)waves_per_wg * (size_t)cfg.dstack_cap * sizeof(int32_t);
         uint32_t epoch = 0;

@@ -29,7 +29,7 @@ EXPORTED = (
     "satmi_dpll_batch_device", "satmi_dpll_batch_host", "satmi_dpll_lds_bytes", "satmi_resolution_host",
     "satmi_dp_host", "satmi_dpll_scan_lds_bytes", "satmi_dpll_set_kernel", "satmi_dpll_plan",
     "satmi_dpll_launch_span", "satmi_wallclock_hz", "satmi_resolution_debug_slot_base",
-    "satmi_resolution_last_stats", "satmi_dpll_set_split",
+    "satmi_resolution_last_stats", "satmi_dpll_set_split", "satmi_dpll_split_stats", "satmi_dp_last_stats",
 )
 
 
@@ -38,9 +38,18 @@ def set_kernel(policy):
     check(load().satmi_dpll_set_kernel(int(policy)), "satmi_dpll_set_kernel")
 
 
-def set_split(enable):
-    """Process-wide branch splitting of the clause kernels' launch tails (default on)."""
-    check(load().satmi_dpll_set_split(int(bool(enable))), "satmi_dpll_set_split")
+def set_split(enable, helpers_per_cu=0):
+    """Process-wide branch splitting of the clause kernels' launch tails (default on;
+    helpers_per_cu 0 = the library default)."""
+    check(load().satmi_dpll_set_split(int(bool(enable)), int(helpers_per_cu)), "satmi_dpll_set_split")
+
+
+def split_stats(stream=None):
+    """Branch-splitting statistics of the last split launch on `stream` (a HIP stream handle)."""
+    out = (ctypes.c_int64 * 7)()
+    check(load().satmi_dpll_split_stats(stream, out), "satmi_dpll_split_stats")
+    keys = ("donations", "tickets", "claims", "reclaims", "helpers", "wait_ticks", "done")
+    return dict(zip(keys, list(out)))
 
 
 class SatmiError(RuntimeError):
@@ -81,7 +90,8 @@ def load():
     L.satmi_dpll_scan_lds_bytes.restype = ctypes.c_uint64
     L.satmi_dpll_scan_lds_bytes.argtypes = [ctypes.c_int] * 4
     L.satmi_dpll_set_kernel.argtypes = [ctypes.c_int]
-    L.satmi_dpll_set_split.argtypes = [ctypes.c_int]
+    L.satmi_dpll_set_split.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.satmi_dpll_split_stats.argtypes = [vp, i64p]
     L.satmi_dpll_launch_span.argtypes = [vp, vp]
     L.satmi_wallclock_hz.argtypes = [P(ctypes.c_double)]
     L.satmi_dpll_plan.argtypes = [ctypes.c_int] * 6 + [P(ctypes.c_int), P(ctypes.c_uint64), P(ctypes.c_int)]
@@ -97,6 +107,7 @@ def load():
         ctypes.c_int, i32p, i32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
         i32p, i32p, i64p, ctypes.c_int, i32p, ctypes.c_int64, i64p, ctypes.c_int64, i64p, ctypes.c_int]
     L.satmi_resolution_debug_slot_base.argtypes = [ctypes.c_int64]
+    L.satmi_dp_last_stats.argtypes = [i64p, i64p, i64p, i64p, P(ctypes.c_int), P(ctypes.c_double)]
     L.satmi_resolution_last_stats.argtypes = [i64p, i64p, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)]
     L.satmi_dp_host.argtypes = [

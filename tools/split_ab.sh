@@ -15,13 +15,11 @@ run() {   # name, args...
   local name=$1; shift
   timeout -k 10 240 python bench.py --no-cpu-baseline "$@" > "$OUT/bench_$name.json" 2> "$OUT/bench_$name.err" \
     || { echo "bench $name failed"; tail -20 "$OUT/bench_$name.err"; exit 1; }
-  python -c "import json,sys; d=json.load(open('$OUT/bench_$name.json')); print('$name', round(d['value']), 'util', round(d['wave_utilisation'],3), 'kernel_ms', round(d['roofline']['kernel_ms'],1))"
+  python -c "import json,sys; d=json.load(open('$OUT/bench_$name.json')); print('$name', round(d['value']), 'util', round(d['wave_utilisation'],3), 'kernel_ms', round(d['roofline']['kernel_ms'],1), d.get('branch_split'))"
 }
 run share_split_s2 --total 32768 --steps 20 --warmup 3
-run share_nosplit_s2 --total 32768 --steps 20 --warmup 3 --no-split
 run share_split_s1 --total 32768 --steps 20 --warmup 3 --streams 1
-run share_nosplit_s1 --total 32768 --steps 20 --warmup 3 --streams 1 --no-split
 run full_split_s2 --steps 10 --warmup 2
 run full_nosplit_s2 --steps 10 --warmup 2 --no-split
-run full_split_s1 --steps 10 --warmup 2 --streams 1
+grep -h -o '"branch_split": {[^}]*}' "$OUT"/bench_*.json
 echo done
