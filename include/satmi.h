@@ -165,6 +165,35 @@ int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_li
 int satmi_dp_last_stats(int64_t *steps, int64_t *subset_tests, int64_t *new_clauses, int64_t *candidate_bytes,
                         int *words, double *subsume_ms);
 
+/*
+ * CDCL, replaces CDCLSolver / cdcl_solve (REF.py:217-384) for a batch of
+ * formulas (CSR host arrays as satmi_dpll_batch_host), one wavefront per
+ * instance.  The reference's solve loop has no bound of its own (its caller
+ * kills it after 60 s): an instance stops after max_iter loop iterations (<= 0:
+ * none), at time_limit_s (<= 0: none) or when its arena (sized for learn_cap
+ * learned clauses; <= 0: max_iter, else 65536) is full.
+ *   h_status[b]   SATMI_CDCL_SAT / _UNSAT (the reference's (True, model) /
+ *                 (False, None)), _LIMIT (a bound stopped it), _ERROR (the
+ *                 reference raises: KeyError in analyze_conflict), _FULL
+ *   h_assign      [B x assign_stride] the assignment dict as signed literals in
+ *                 its insertion order (h_assign_len[b] of them): the model for
+ *                 _SAT, else the live dict where the run stopped
+ *   h_stats       [B x SATMI_CDCL_NSTATS] iterations, conflicts analysed,
+ *                 decisions, learned clauses, formula length, watch-list keys,
+ *                 decision level, set-table slots used
+ *   h_var_inc[b]  the solver's var_inc at the end
+ */
+#define SATMI_CDCL_UNSAT 0
+#define SATMI_CDCL_SAT 1
+#define SATMI_CDCL_LIMIT (-1)
+#define SATMI_CDCL_ERROR (-2)
+#define SATMI_CDCL_FULL (-3)
+#define SATMI_CDCL_NSTATS 8
+int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_clause_begin, const int32_t *h_clause_lit_begin,
+                          const int32_t *h_lits, int64_t max_iter, int64_t learn_cap, double time_limit_s,
+                          int32_t *h_status, int32_t *h_assign_len, int32_t *h_assign, int assign_stride,
+                          int64_t *h_stats, double *h_var_inc);
+
 /* Device-side span of the last DPLL launch on `stream`: enqueues (on that
  * stream, after the launch) a copy of two uint64 s_memrealtime ticks into
  * d_span: [0] = ~(first wave's start), [1] = last wave's end, so the launch
@@ -206,7 +235,7 @@ int satmi_dpll_set_kernel(int policy);
  * cancelled and count nothing).  Applies to SOUND-mode launches with
  * max_solutions == 1, no node limit and no time limit.
  *   helpers_per_cu  wavefronts per CU that stay as helpers once the queue
- *                   drains (0 = default 4); the others exit, freeing their CU
+ *                   drains (0 = default 1); the others exit, freeing their CU
  *                   slots for a launch queued on another stream */
 int satmi_dpll_set_split(int enable, int helpers_per_cu);
 

@@ -42,6 +42,9 @@ def lib():
         L.oracle_resolution.argtypes = [ctypes.c_int, i32p, i32p, ctypes.c_int, ctypes.c_int64, i64p,
                                         ctypes.c_int, P(ctypes.c_int), i32p, ctypes.c_int64, i64p,
                                         ctypes.c_int64, i64p, ctypes.c_int]
+        L.oracle_cdcl.restype = ctypes.c_int
+        L.oracle_cdcl.argtypes = [ctypes.c_int, i32p, i32p, ctypes.c_int64, i32p, P(ctypes.c_int32), i64p,
+                                  P(ctypes.c_double)]
         L.pyset_probe_from_list.restype = ctypes.c_int
         L.pyset_probe_from_list.argtypes = [i64p, ctypes.c_int, i64p]
         L.pyset_probe_resolvent.restype = ctypes.c_int
@@ -160,3 +163,23 @@ def pyset_var_pop(lists):
         off[i + 1] = off[i] + len(c)
     lits = np.array([l for c in lists for l in c] or [0], dtype=np.int64)
     return lib().pyset_probe_var_pop(_p(lits, ctypes.c_int64), _p(off, ctypes.c_int), len(lists))
+
+
+CDCL_STATS = ("iterations", "conflicts", "decisions", "learned", "clauses", "watch_keys", "level")
+
+
+def cdcl(formula, max_iter=0):
+    """cdcl_solve (REF.py:382-384) restated: {"result": 1 True | 0 False | -1 the
+    iteration cap | -2 the reference raises, "assignment": the assignment dict as
+    signed literals in insertion order (the model for result 1), "var_inc",
+    "stats": CDCL_STATS}."""
+    off, lits = _csr(formula)
+    nv = max([abs(l) for c in formula for l in c] + [1])
+    model = np.zeros(nv + 1, dtype=np.int32)
+    mlen = ctypes.c_int32(0)
+    st = np.zeros(len(CDCL_STATS), dtype=np.int64)
+    vi = ctypes.c_double(0.0)
+    r = lib().oracle_cdcl(len(formula), _p(off), _p(lits), int(max_iter), _p(model), ctypes.byref(mlen),
+                          _p(st, ctypes.c_int64), ctypes.byref(vi))
+    return {"result": r, "assignment": model[:mlen.value].tolist(), "var_inc": vi.value,
+            "stats": dict(zip(CDCL_STATS, st.tolist()))}

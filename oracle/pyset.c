@@ -98,6 +98,7 @@ found_unused:
 }
 
 void pyset_add(pyset *s, int64_t key) { add_entry(s, key, py_hash_int(key)); }
+void pyset_add_hashed(pyset *s, int64_t key, int64_t hash) { add_entry(s, key, hash); }
 
 int pyset_contains(const pyset *s, int64_t key) {
     int64_t hash = py_hash_int(key);
@@ -153,8 +154,14 @@ void pyset_copy(pyset *dst, const pyset *src) {
     merge(dst, src);
 }
 
-static void discard(pyset *s, int64_t key) {
-    int64_t hash = py_hash_int(key);
+static void discard_hashed(pyset *s, int64_t key, int64_t hash);
+static void discard(pyset *s, int64_t key) { discard_hashed(s, key, py_hash_int(key)); }
+int pyset_discard_hashed(pyset *s, int64_t key, int64_t hash) {
+    const int64_t before = s->used;
+    discard_hashed(s, key, hash);
+    return s->used < before;
+}
+static void discard_hashed(pyset *s, int64_t key, int64_t hash) {
     uint64_t mask = (uint64_t)s->mask, i = (uint64_t)hash & mask, perturb = (uint64_t)hash;
     pyentry *e = &s->table[i];
     if (e->key == 0) return;

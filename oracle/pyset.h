@@ -34,6 +34,10 @@ typedef struct {
 void pyset_init(pyset *s);                        /* empty set (8 slots) */
 void pyset_free(pyset *s);
 void pyset_add(pyset *s, int64_t key);            /* set_add_key          */
+/* the same with the caller's hash: keys stored as x + 1 (0 marks an unused slot)
+ * for non-negative ints x, whose CPython hash is x */
+void pyset_add_hashed(pyset *s, int64_t key, int64_t hash);
+int  pyset_discard_hashed(pyset *s, int64_t key, int64_t hash);   /* 1 if it was present */
 int  pyset_contains(const pyset *s, int64_t key); /* `key in s`           */
 void pyset_from_array(pyset *s, const int64_t *keys, int n);   /* set(list)  */
 void pyset_copy(pyset *dst, const pyset *src);    /* set_copy / make_new_set(src) */

@@ -1,0 +1,770 @@
+// cdcl.hip -- the reference's CDCLSolver / cdcl_solve (REF.py:217-384) on gfx950,
+// batched: one wavefront per instance, the solver state in a per-wave HBM arena.
+//
+// The reference's search is decided by the iteration order of its Python
+// containers, so the kernel keeps their layouts, not just their contents:
+//   * watch_list (defaultdict(set), REF.py:227): the keys in insertion order
+//     (klit[]), each value a CPython 3.10 set table of clause indices -- int
+//     keys i hash to i, stored as i + 1 (0 = an unused slot, INT32_MIN = a
+//     dummy); add / discard / resize follow Objects/setobject.c (set_add_entry,
+//     set_discard_entry, set_table_resize, set_insert_clean), so
+//     `list(self.watch_list[lit])` (REF.py:276) iterates in the reference's order;
+//   * assignment (dict, REF.py:222): a value and an insertion stamp per
+//     variable; a deleted key re-enters last (REF.py:362), the model comes out
+//     in stamp order (REF.py:258, :262);
+//   * activity / var_inc: IEEE double arithmetic in the reference's order
+//     (REF.py:355-357, :378), max() keeping the first maximal variable.
+// What runs across the wave's 64 lanes (everything else is lane 0):
+//   * propagate (REF.py:269-304): per false watch literal, the set's table is
+//     compacted into its iteration-order snapshot by ballots; the replacement
+//     watch of every snapshot clause (its first other literal that is free or
+//     true) is found one clause per lane; the first clause without one is the
+//     conflict; the snapshot's removals are dummy marks at known slots (no
+//     resize on discard), the adds go in order on lane 0 (they may create keys);
+//   * the all-assigned test (REF.py:257) over a bitmap of the variables that
+//     occur; select_variable's max over activities (REF.py:370-379);
+//     backtracking (REF.py:359-368); the model's dict order (a rank per stamp).
+// The solve loop (REF.py:247-267) has no bound in the reference (its caller
+// kills it after 60 s, REF.py:417-437): here a launch stops an instance after
+// max_iter iterations, at its time limit, or when its arena is full.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <vector>
+
+#include "common.h"
+
+namespace satmi {
+namespace {
+
+constexpr int32_t WS_EMPTY = 0, WS_DUMMY = INT32_MIN;
+constexpr int WS_MINSIZE = 8, WS_PROBES = 9, WS_PERTURB = 5;
+constexpr int64_t ANTE_ABSENT = -2;
+constexpr double VAR_DECAY = 0.95;
+
+enum { CD_FALSE = 0, CD_TRUE = 1, CD_LIMIT = -1, CD_ERROR = -2, CD_FULL = -3 };
+
+// Per-wave arena layout (offsets in bytes), sized on the host for the batch.
+struct CdclLayout {
+    uint64_t coff, lits, val, ord, lev, ante, act, appears, klit, kidx, woff, wmask, wfill, wused, pool, snap, rep,
+        slot, scratch, bytes;
+    int64_t clause_cap, lit_cap, pool_cap, snap_cap;
+    int32_t ncap;   // variables
+};
+
+struct CdclArgs {
+    const int32_t *inst_clause_begin, *clause_lit_begin, *lits, *inst_nvars;
+    int32_t num_instances;
+    int64_t max_iter;
+    uint64_t time_limit_ticks;
+    int32_t *status, *assign_len, *assign;   // assign: [B x assign_stride] signed literals, dict order
+    int32_t assign_stride;
+    int64_t *stats;                          // [B x CDCL_NSTATS]
+    double *var_inc;                         // [B]
+    unsigned char *arena;
+    CdclLayout lay;
+    uint32_t *work_counter;
+};
+
+struct St {   // views into one wave's arena
+    int64_t *coff;
+    int32_t *lits;
+    int8_t *val;
+    int64_t *ord;
+    int32_t *lev;
+    int64_t *ante;
+    double *act;
+    uint64_t *appears;
+    int32_t *klit, *kidx;
+    int64_t *woff;
+    int32_t *wmask, *wfill, *wused;
+    int32_t *pool, *snap, *rep, *slot, *scratch;
+};
+
+__device__ __forceinline__ int iabs(int x) { return x < 0 ? -x : x; }
+__device__ __forceinline__ int lcode(int lit) { return (iabs(lit) << 1) | (lit < 0 ? 1 : 0); }
+
+// Lane-0 state of the sequential parts, mirrored to every lane by broadcasts.
+struct Seq {
+    int64_t nf;        // formula length (clauses)
+    int64_t nlits;     // literals stored
+    int64_t pool_top;  // set-table pool in use (slots)
+    int32_t nk;        // watch-list keys
+    int64_t next_ord;
+    int32_t level;
+    double var_inc;
+    bool full;         // the arena ran out
+};
+
+__device__ bool ws_alloc(const CdclArgs &A, Seq &q, int64_t slots, int64_t *off) {
+    if (q.pool_top + slots > A.lay.pool_cap) {
+        q.full = true;
+        return false;
+    }
+    *off = q.pool_top;
+    q.pool_top += slots;
+    return true;
+}
+
+__device__ void ws_insert_clean(int32_t *t, uint64_t mask, int32_t key) {
+    const uint64_t h = (uint64_t)(int64_t)(key - 1);
+    uint64_t perturb = h, i = h & mask;
+    for (;;) {
+        if (t[i] == WS_EMPTY) {
+            t[i] = key;
+            return;
+        }
+        if (i + WS_PROBES <= mask)
+            for (int j = 1; j <= WS_PROBES; ++j)
+                if (t[i + j] == WS_EMPTY) {
+                    t[i + j] = key;
+                    return;
+                }
+        perturb >>= WS_PERTURB;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+// set_table_resize(so, minused)  (lane 0)
+__device__ void ws_resize(const CdclArgs &A, const St &S, Seq &q, int k, int64_t minused) {
+    int64_t newsize = WS_MINSIZE;
+    while (newsize <= minused) newsize <<= 1;
+    const int32_t mask = S.wmask[k];
+    if (newsize == WS_MINSIZE && mask == WS_MINSIZE - 1 && S.wfill[k] == S.wused[k]) return;
+    int64_t off;
+    if (!ws_alloc(A, q, newsize, &off)) return;
+    int32_t *nt = S.pool + off, *ot = S.pool + S.woff[k];
+    for (int64_t i = 0; i < newsize; ++i) nt[i] = WS_EMPTY;
+    for (int64_t i = 0; i <= mask; ++i)
+        if (ot[i] != WS_EMPTY && ot[i] != WS_DUMMY) ws_insert_clean(nt, (uint64_t)(newsize - 1), ot[i]);
+    S.woff[k] = off;
+    S.wmask[k] = (int32_t)(newsize - 1);
+    S.wfill[k] = S.wused[k];
+}
+
+// set_add_entry(so, key, hash = key - 1)  (lane 0)
+__device__ void ws_add(const CdclArgs &A, const St &S, Seq &q, int k, int32_t key) {
+    const int64_t h = (int64_t)(key - 1);
+    int32_t *t = S.pool + S.woff[k];
+    const uint64_t mask = (uint64_t)S.wmask[k];
+    uint64_t i = (uint64_t)h & mask;
+    int64_t slot = (int64_t)i;
+    if (t[i] != WS_EMPTY) {
+        int64_t freeslot = -1;
+        uint64_t perturb = (uint64_t)h;
+        for (;;) {
+            int32_t x = t[i];
+            if (x == key) return;
+            if (x == WS_DUMMY) freeslot = (int64_t)i;   // CPython 3.10 keeps the LAST dummy probed
+            bool hit_empty = false;
+            if (i + WS_PROBES <= mask) {
+                for (int j = 1; j <= WS_PROBES; ++j) {
+                    x = t[i + j];
+                    if (x == WS_EMPTY) {
+                        slot = (int64_t)(i + j);
+                        hit_empty = true;
+                        break;
+                    }
+                    if (x == key) return;
+                    if (x == WS_DUMMY) freeslot = (int64_t)(i + j);
+                }
+            }
+            if (!hit_empty) {
+                perturb >>= WS_PERTURB;
+                i = (i * 5 + 1 + perturb) & mask;
+                if (t[i] != WS_EMPTY) continue;
+                slot = (int64_t)i;
+            }
+            if (freeslot >= 0) {   // found_unused_or_dummy with a dummy on the way
+                S.wused[k]++;
+                t[freeslot] = key;
+                return;
+            }
+            break;
+        }
+    }
+    S.wfill[k]++;
+    S.wused[k]++;
+    t[slot] = key;
+    if ((uint64_t)S.wfill[k] * 5 < mask * 3) return;
+    const int64_t used = S.wused[k];
+    ws_resize(A, S, q, k, used > 50000 ? used * 2 : used * 4);
+}
+
+// self.watch_list[lit] (defaultdict: a missing key is created with an empty set)  (lane 0)
+__device__ int key_of(const CdclArgs &A, const St &S, Seq &q, int lit) {
+    const int c = lcode(lit);
+    int k = S.kidx[c] - 1;
+    if (k >= 0) return k;
+    int64_t off;
+    if (!ws_alloc(A, q, WS_MINSIZE, &off)) return -1;
+    k = q.nk++;
+    S.klit[k] = lit;
+    S.kidx[c] = k + 1;
+    S.woff[k] = off;
+    S.wmask[k] = WS_MINSIZE - 1;
+    S.wfill[k] = S.wused[k] = 0;
+    for (int i = 0; i < WS_MINSIZE; ++i) S.pool[off + i] = WS_EMPTY;
+    return k;
+}
+
+__device__ void watch_add(const CdclArgs &A, const St &S, Seq &q, int lit, int64_t idx) {
+    const int k = key_of(A, S, q, lit);
+    if (k >= 0 && !q.full) ws_add(A, S, q, k, (int32_t)(idx + 1));
+}
+
+__device__ __forceinline__ bool lit_false(const St &S, int lit) {
+    const int8_t v = S.val[iabs(lit)];
+    return v >= 0 && (lit > 0) != (v != 0);
+}
+
+// Broadcast lane 0's Seq to the wave (after lane-0 sections).
+__device__ void sync_seq(Seq &q) {
+    wave_sync();
+    q.nf = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q.nf) |
+           ((int64_t)__builtin_amdgcn_readfirstlane((int)(q.nf >> 32)) << 32);
+    q.nlits = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q.nlits) |
+              ((int64_t)__builtin_amdgcn_readfirstlane((int)(q.nlits >> 32)) << 32);
+    q.pool_top = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q.pool_top) |
+                 ((int64_t)__builtin_amdgcn_readfirstlane((int)(q.pool_top >> 32)) << 32);
+    q.next_ord = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q.next_ord) |
+                 ((int64_t)__builtin_amdgcn_readfirstlane((int)(q.next_ord >> 32)) << 32);
+    q.nk = __builtin_amdgcn_readfirstlane(q.nk);
+    q.level = __builtin_amdgcn_readfirstlane(q.level);
+    const uint64_t vb = __double_as_longlong(q.var_inc);
+    q.var_inc = __longlong_as_double((long long)((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)vb) |
+                                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(vb >> 32))
+                                                  << 32)));
+    q.full = __builtin_amdgcn_readfirstlane((int)q.full) != 0;
+}
+
+// propagate (REF.py:269-304): returns the conflict clause's index, -1 for none.
+// (The reference's unit branch, REF.py:290-291 / :297-304, needs a watched
+// clause of length 1; watched clauses are longer than 1 (REF.py:235, :351),
+// so its pass ends either at a conflict or with `unit is None`.)
+__device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const int nk0 = q.nk;   // list(self.watch_list): keys created during the pass are not visited
+    for (int k0 = 0; k0 < nk0; k0 += 64) {
+        const int kk = k0 + ln;
+        const bool fl = kk < nk0 && lit_false(S, S.klit[kk]);
+        uint64_t fm = __ballot(fl);
+        while (fm) {
+            const int ki = k0 + __builtin_ctzll(fm);
+            fm &= fm - 1;
+            const int lit = S.klit[ki];
+            // snapshot of the set in iteration order (table slot order), with slots
+            const int32_t *t = S.pool + S.woff[ki];
+            const int32_t mask = S.wmask[ki];
+            int n = 0;
+            for (int i0 = 0; i0 <= mask; i0 += 64) {
+                const int i = i0 + ln;
+                const int32_t x = i <= mask ? t[i] : WS_EMPTY;
+                const bool act = x != WS_EMPTY && x != WS_DUMMY;
+                const uint64_t am = __ballot(act);
+                if (act) {
+                    const int p = n + __popcll(am & lt);
+                    S.snap[p] = x - 1;
+                    S.slot[p] = i;
+                }
+                n += __popcll(am);
+            }
+            wave_sync();
+            // replacement watch per snapshot clause, one clause per lane
+            int64_t conflict = -1;
+            int upto = n;   // snapshot entries whose watch moves (before the conflict)
+            for (int p0 = 0; p0 < n; p0 += 64) {
+                const int p = p0 + ln;
+                int r = 0;
+                bool none = false;
+                if (p < n) {
+                    const int64_t c = S.snap[p];
+                    const int64_t jb = S.coff[c], je = S.coff[c + 1];
+                    for (int64_t j = jb; j < je; ++j) {
+                        const int o = S.lits[j];
+                        if (o == lit) continue;
+                        const int8_t v = S.val[iabs(o)];
+                        if (v < 0 || (o > 0) == (v != 0)) {
+                            r = o;
+                            break;
+                        }
+                    }
+                    none = r == 0;
+                    S.rep[p] = r;
+                }
+                const uint64_t nm = __ballot(none);
+                if (nm) {
+                    upto = p0 + __builtin_ctzll(nm);
+                    conflict = S.snap[upto];
+                    break;
+                }
+            }
+            wave_sync();
+            conflict = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)conflict) |
+                       ((int64_t)__builtin_amdgcn_readfirstlane((int)(conflict >> 32)) << 32);
+            upto = __builtin_amdgcn_readfirstlane(upto);
+            // self.watch_list[lit].remove(idx): dummies at the snapshot's slots
+            int32_t *tw = S.pool + S.woff[ki];
+            for (int p = ln; p < upto; p += 64) tw[S.slot[p]] = WS_DUMMY;
+            if (ln == 0) {
+                S.wused[ki] -= upto;
+                // self.watch_list[other_lit].add(idx), in snapshot order
+                for (int p = 0; p < upto && !q.full; ++p) watch_add(A, S, q, S.rep[p], S.snap[p]);
+            }
+            sync_seq(q);
+            if (conflict >= 0 || q.full) return conflict;
+        }
+    }
+    return -1;
+}
+
+// analyze_conflict (REF.py:306-345) on lane 0: learned literals into S.scratch
+// (returns their count), the backtrack level into *bt; -1 where the reference
+// raises KeyError (an unassigned variable reaching self.levels[...]).
+__device__ int analyze_conflict(const St &S, int64_t conflict, int32_t cap, int32_t *bt) {
+    const int64_t jb = S.coff[conflict], je = S.coff[conflict + 1];
+    int32_t *L = S.scratch;
+    int n = 0;
+    for (int64_t j = jb; j < je; ++j) {
+        if (S.val[iabs(S.lits[j])] < 0) return -1;
+        L[n++] = S.lits[j];
+    }
+    for (;;) {
+        int mx = -1, sc = -1, d = 0;
+        for (int i = 0; i < n; ++i) {
+            const int l = S.lev[iabs(L[i])];
+            bool seen = false;
+            for (int j = 0; j < i; ++j) seen |= S.lev[iabs(L[j])] == l;
+            if (seen) continue;
+            ++d;
+            if (l > mx) {
+                sc = mx;
+                mx = l;
+            } else if (l > sc) {
+                sc = l;
+            }
+        }
+        bool stop = d <= 1;
+        int last = 0;
+        if (!stop) {
+            for (int i = 0; i < n; ++i)
+                if (S.lev[iabs(L[i])] == mx) {
+                    last = L[i];
+                    break;
+                }
+            stop = last == 0 || S.ante[iabs(last)] < 0;   // None or -1
+        }
+        if (stop) {
+            *bt = d > 1 ? sc : 0;
+            return n;
+        }
+        // resolve with the antecedent (REF.py:331-342): new list in scratch + cap
+        const int64_t a = S.ante[iabs(last)];
+        const int64_t ab = S.coff[a], ae = S.coff[a + 1];
+        int32_t *N = L + cap;
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            bool neg_in = false;
+            for (int64_t j = ab; j < ae; ++j) neg_in |= S.lits[j] == -L[i];
+            if (L[i] != last && !neg_in) N[m++] = L[i];
+        }
+        for (int64_t j = ab; j < ae; ++j) {
+            const int x = S.lits[j];
+            bool in_new = false;
+            for (int i = 0; i < m; ++i) in_new |= N[i] == x;
+            if (x != -last && !in_new && m < cap) N[m++] = x;
+        }
+        for (int i = 0; i < m; ++i) {
+            if (S.val[iabs(N[i])] < 0) return -1;
+            L[i] = N[i];
+        }
+        n = m;
+    }
+}
+
+__device__ void solve_one(const CdclArgs &A, const St &S, int b) {
+    const int ln = lane_id();
+    const int cb = A.inst_clause_begin[b], ce = A.inst_clause_begin[b + 1];
+    const int m = ce - cb;
+    const int lb = A.clause_lit_begin[cb], le = A.clause_lit_begin[ce];
+    const int n = A.inst_nvars[b];
+    int64_t *st = A.stats + (int64_t)b * SATMI_CDCL_NSTATS;
+    int status = CD_LIMIT;
+    if (m > A.lay.clause_cap || (le - lb) > A.lay.lit_cap || n > A.lay.ncap) {
+        status = CD_FULL;
+        if (ln == 0) {
+            A.status[b] = status;
+            A.assign_len[b] = 0;
+            for (int i = 0; i < SATMI_CDCL_NSTATS; ++i) st[i] = 0;
+            A.var_inc[b] = 1.0;
+        }
+        return;
+    }
+    // ---- stage: formula, empty dicts
+    for (int i = ln; i <= m; i += 64) S.coff[i] = A.clause_lit_begin[cb + i] - lb;
+    for (int i = ln; i < le - lb; i += 64) S.lits[i] = A.lits[lb + i];
+    for (int v = ln; v <= n; v += 64) {
+        S.val[v] = -1;
+        S.ante[v] = ANTE_ABSENT;
+        S.act[v] = 0.0;
+        S.lev[v] = 0;
+        S.ord[v] = 0;
+        S.kidx[2 * v] = S.kidx[2 * v + 1] = 0;
+    }
+    for (int w = ln; w <= (n >> 6); w += 64) S.appears[w] = 0ull;
+    wave_sync();
+    for (int i = ln; i < le - lb; i += 64) {
+        const int v = iabs(S.lits[i]);
+        atomicOr((unsigned long long *)&S.appears[v >> 6], 1ull << (v & 63));
+    }
+    wave_sync();
+    Seq q;
+    q.nf = m;
+    q.nlits = le - lb;
+    q.pool_top = 0;
+    q.nk = 0;
+    q.next_ord = 0;
+    q.level = 0;
+    q.var_inc = 1.0;
+    q.full = false;
+    // setup_watch_list (REF.py:233-244)
+    if (ln == 0) {
+        for (int64_t i = 0; i < m && !q.full; ++i) {
+            const int64_t jb = S.coff[i], len = S.coff[i + 1] - jb;
+            if (len > 1) {
+                watch_add(A, S, q, S.lits[jb], i);
+                watch_add(A, S, q, S.lits[jb + 1], i);
+            } else if (len == 1) {
+                const int x = S.lits[jb], v = iabs(x);
+                if (S.val[v] < 0) {
+                    S.val[v] = x > 0;
+                    S.ord[v] = q.next_ord++;
+                    S.lev[v] = 0;
+                    S.ante[v] = i;
+                }
+            }
+        }
+    }
+    sync_seq(q);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int64_t it = 0, conflicts = 0, decisions = 0, learned = 0;
+    while (!q.full) {
+        if (A.max_iter > 0 && it >= A.max_iter) break;
+        if (A.time_limit_ticks && __builtin_amdgcn_s_memrealtime() - t0 > A.time_limit_ticks) break;
+        ++it;
+        const int64_t conflict = propagate(A, S, q);
+        if (q.full) break;
+        if (conflict >= 0) {
+            if (q.level == 0) {
+                status = CD_FALSE;
+                break;
+            }
+            ++conflicts;
+            int32_t cnt = 0, bt = 0;
+            if (ln == 0) {
+                cnt = analyze_conflict(S, conflict, A.lay.ncap * 2 + 2, &bt);
+                if (cnt > 0) {   // learn_clause (REF.py:347-357)
+                    if (q.nf + 1 > A.lay.clause_cap || q.nlits + cnt > A.lay.lit_cap) {
+                        q.full = true;
+                    } else {
+                        const int64_t idx = q.nf;
+                        for (int i = 0; i < cnt; ++i) S.lits[q.nlits + i] = S.scratch[i];
+                        q.nlits += cnt;
+                        S.coff[idx + 1] = q.nlits;
+                        q.nf = idx + 1;
+                        if (cnt > 1) {
+                            watch_add(A, S, q, S.scratch[0], idx);
+                            watch_add(A, S, q, S.scratch[1], idx);
+                        }
+                        q.var_inc *= 1.0 / VAR_DECAY;
+                        for (int i = 0; i < cnt; ++i) S.act[iabs(S.scratch[i])] += q.var_inc;
+                    }
+                }
+            }
+            sync_seq(q);
+            cnt = __builtin_amdgcn_readfirstlane(cnt);
+            bt = __builtin_amdgcn_readfirstlane(bt);
+            if (cnt < 0) {
+                status = CD_ERROR;
+                break;
+            }
+            if (q.full) break;
+            learned += cnt > 0 ? 1 : 0;
+            // backtrack (REF.py:359-368)
+            for (int v = 1 + ln; v <= n; v += 64)
+                if (S.val[v] >= 0 && S.lev[v] > bt) {
+                    S.val[v] = -1;
+                    S.ante[v] = ANTE_ABSENT;
+                }
+            q.level = bt;
+            wave_sync();
+        } else {
+            // all(abs(l) in self.assignment ...) (REF.py:257)
+            bool miss = false;
+            for (int v = 1 + ln; v <= n; v += 64)
+                miss |= ((S.appears[v >> 6] >> (v & 63)) & 1ull) && S.val[v] < 0;
+            if (!__ballot(miss)) {
+                status = CD_TRUE;
+                break;
+            }
+            // select_variable (REF.py:370-379): the first unassigned variable of
+            // maximal activity among 1..max(abs(l)); n is that maximum
+            double best = -1.0;
+            int bv = INT_MAX;
+            for (int v = 1 + ln; v <= n; v += 64)
+                if (S.val[v] < 0 && (bv == INT_MAX || S.act[v] > best)) {
+                    best = S.act[v];
+                    bv = v;
+                }
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double ob = __shfl_xor(best, off, 64);
+                const int ov = __shfl_xor(bv, off, 64);
+                if (ov != INT_MAX && (bv == INT_MAX || ob > best || (ob == best && ov < bv))) {
+                    best = ob;
+                    bv = ov;
+                }
+            }
+            bv = __builtin_amdgcn_readfirstlane(bv);
+            if (bv == INT_MAX) {   // no unassigned variable: True (REF.py:261-262)
+                status = CD_TRUE;
+                break;
+            }
+            q.var_inc *= VAR_DECAY;
+            q.level += 1;
+            ++decisions;
+            if (ln == 0) {
+                S.val[bv] = 1;
+                S.ord[bv] = q.next_ord++;
+                S.lev[bv] = q.level;
+                S.ante[bv] = ANTE_ABSENT;
+            }
+            sync_seq(q);
+        }
+    }
+    if (q.full) status = CD_FULL;
+    // the assignment dict in insertion order: rank every assigned variable by stamp
+    int na = 0;
+    for (int v = 1 + ln; v <= n; v += 64) na += S.val[v] >= 0 ? 1 : 0;
+    for (int off = 32; off >= 1; off >>= 1) na += __shfl_xor(na, off, 64);
+    int32_t *out = A.assign + (int64_t)b * A.assign_stride;
+    for (int v = 1 + ln; v <= n; v += 64) {
+        if (S.val[v] < 0) continue;
+        int r = 0;
+        for (int u = 1; u <= n; ++u) r += (S.val[u] >= 0 && S.ord[u] < S.ord[v]) ? 1 : 0;
+        if (r < A.assign_stride) out[r] = S.val[v] ? v : -v;
+    }
+    if (ln == 0) {
+        A.status[b] = status;
+        A.assign_len[b] = min(na, A.assign_stride);
+        st[0] = it;
+        st[1] = conflicts;
+        st[2] = decisions;
+        st[3] = learned;
+        st[4] = q.nf;
+        st[5] = q.nk;
+        st[6] = q.level;
+        st[7] = q.pool_top;
+        A.var_inc[b] = q.var_inc;
+    }
+}
+
+__global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
+    unsigned char *base = A.arena + (size_t)blockIdx.x * (size_t)A.lay.bytes;
+    St S;
+    S.coff = (int64_t *)(base + A.lay.coff);
+    S.lits = (int32_t *)(base + A.lay.lits);
+    S.val = (int8_t *)(base + A.lay.val);
+    S.ord = (int64_t *)(base + A.lay.ord);
+    S.lev = (int32_t *)(base + A.lay.lev);
+    S.ante = (int64_t *)(base + A.lay.ante);
+    S.act = (double *)(base + A.lay.act);
+    S.appears = (uint64_t *)(base + A.lay.appears);
+    S.klit = (int32_t *)(base + A.lay.klit);
+    S.kidx = (int32_t *)(base + A.lay.kidx);
+    S.woff = (int64_t *)(base + A.lay.woff);
+    S.wmask = (int32_t *)(base + A.lay.wmask);
+    S.wfill = (int32_t *)(base + A.lay.wfill);
+    S.wused = (int32_t *)(base + A.lay.wused);
+    S.pool = (int32_t *)(base + A.lay.pool);
+    S.snap = (int32_t *)(base + A.lay.snap);
+    S.rep = (int32_t *)(base + A.lay.rep);
+    S.slot = (int32_t *)(base + A.lay.slot);
+    S.scratch = (int32_t *)(base + A.lay.scratch);
+    span_begin(A.work_counter);
+    for (;;) {
+        uint32_t b = 0;
+        if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
+        b = uniform_u32(b);
+        if (b >= (uint32_t)A.num_instances) break;
+        solve_one(A, S, (int)b);
+        wave_sync();
+    }
+    span_end(A.work_counter);
+}
+
+bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int max_len, int64_t learn_cap,
+                      CdclLayout *L) {
+    const int64_t N = (int64_t)max_vars + 1;
+    const int64_t C = max_clauses + learn_cap;               // clauses incl. learned
+    const int64_t Lc = max_lits + learn_cap * (int64_t)std::max(max_len, 1);
+    const int64_t K = 2 * N;                                 // watch-list keys
+    // set tables: each clause sits in <= 2 sets; a table is < 8x its entries
+    // over its lifetime (doubling tables, dummies until the next resize)
+    const int64_t P = 16 * 2 * C + (int64_t)WS_MINSIZE * K;
+    const int64_t SN = 2 * C + 64;                           // largest snapshot
+    auto a = [](uint64_t x) { return (x + 255u) & ~(uint64_t)255u; };
+    uint64_t o = 0;
+    L->coff = o;    o = a(o + 8 * (uint64_t)(C + 1));
+    L->lits = o;    o = a(o + 4 * (uint64_t)Lc);
+    L->val = o;     o = a(o + (uint64_t)N);
+    L->ord = o;     o = a(o + 8 * (uint64_t)N);
+    L->lev = o;     o = a(o + 4 * (uint64_t)N);
+    L->ante = o;    o = a(o + 8 * (uint64_t)N);
+    L->act = o;     o = a(o + 8 * (uint64_t)N);
+    L->appears = o; o = a(o + 8 * (uint64_t)(N / 64 + 1));
+    L->klit = o;    o = a(o + 4 * (uint64_t)K);
+    L->kidx = o;    o = a(o + 4 * (uint64_t)K);
+    L->woff = o;    o = a(o + 8 * (uint64_t)K);
+    L->wmask = o;   o = a(o + 4 * (uint64_t)K);
+    L->wfill = o;   o = a(o + 4 * (uint64_t)K);
+    L->wused = o;   o = a(o + 4 * (uint64_t)K);
+    L->pool = o;    o = a(o + 4 * (uint64_t)P);
+    L->snap = o;    o = a(o + 4 * (uint64_t)SN);
+    L->rep = o;     o = a(o + 4 * (uint64_t)SN);
+    L->slot = o;    o = a(o + 4 * (uint64_t)SN);
+    L->scratch = o; o = a(o + 4 * (uint64_t)(4 * N + 8));   // two learned-literal lists of <= 2N
+    L->bytes = o;
+    L->clause_cap = C;
+    L->lit_cap = Lc;
+    L->pool_cap = P;
+    L->snap_cap = SN;
+    L->ncap = max_vars;
+    return max_vars >= 0 && max_vars < (1 << 29);
+}
+
+}  // namespace
+}  // namespace satmi
+
+using namespace satmi;
+
+extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_clause_begin,
+                                     const int32_t *h_clause_lit_begin, const int32_t *h_lits, int64_t max_iter,
+                                     int64_t learn_cap, double time_limit_s, int32_t *h_status,
+                                     int32_t *h_assign_len, int32_t *h_assign, int assign_stride,
+                                     int64_t *h_stats, double *h_var_inc) {
+    if (num_instances < 0 || !h_inst_clause_begin || !h_clause_lit_begin || !h_status || !h_assign_len ||
+        !h_assign || !h_stats || !h_var_inc || assign_stride < 0) {
+        set_error("satmi_cdcl_batch_host: bad arguments");
+        return SATMI_ERR_ARG;
+    }
+    if (num_instances == 0) return SATMI_OK;
+    const int C = h_inst_clause_begin[num_instances];
+    const int Ltot = h_clause_lit_begin[C];
+    std::vector<int32_t> nv(num_instances, 0);
+    int max_vars = 0, max_len = 0;
+    int64_t max_clauses = 0, max_lits = 0;
+    for (int b = 0; b < num_instances; ++b) {
+        const int cb = h_inst_clause_begin[b], ce = h_inst_clause_begin[b + 1];
+        max_clauses = std::max<int64_t>(max_clauses, ce - cb);
+        max_lits = std::max<int64_t>(max_lits, h_clause_lit_begin[ce] - h_clause_lit_begin[cb]);
+        for (int c = cb; c < ce; ++c) {
+            max_len = std::max(max_len, h_clause_lit_begin[c + 1] - h_clause_lit_begin[c]);
+            for (int j = h_clause_lit_begin[c]; j < h_clause_lit_begin[c + 1]; ++j) {
+                if (h_lits[j] == 0 || h_lits[j] == INT32_MIN) {
+                    set_error("satmi_cdcl_batch_host: literal 0 / INT32_MIN");
+                    return SATMI_ERR_ARG;
+                }
+                nv[b] = std::max(nv[b], std::abs(h_lits[j]));
+            }
+        }
+        max_vars = std::max(max_vars, nv[b]);
+    }
+    if (assign_stride < max_vars) {
+        set_error("satmi_cdcl_batch_host: assign_stride < number of variables");
+        return SATMI_ERR_ARG;
+    }
+    // learned clauses: one per conflict, at most one per iteration
+    if (learn_cap <= 0) learn_cap = max_iter > 0 ? max_iter : (1 << 16);
+    CdclLayout lay;
+    if (!make_cdcl_layout(max_vars, max_clauses, max_lits, max_len, learn_cap, &lay)) {
+        set_error("satmi_cdcl_batch_host: instance too large");
+        return SATMI_ERR_TOO_LARGE;
+    }
+    int dev = 0, cus = 256;
+    SATMI_HIP(hipGetDevice(&dev));
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    size_t free_b = 0, total_b = 0;
+    SATMI_HIP(hipMemGetInfo(&free_b, &total_b));
+    const size_t by_mem = (free_b / 2) / std::max<uint64_t>(lay.bytes, 1);
+    if (by_mem < 1) {
+        set_error("satmi_cdcl_batch_host: one instance's arena exceeds half the free device memory");
+        return SATMI_ERR_NOMEM;
+    }
+    const int grid = (int)std::min<size_t>({(size_t)num_instances, (size_t)cus * 32, by_mem});
+    int wclock = 0;
+    double ticks_per_s = 1e8;
+    if (hipDeviceGetAttribute(&wclock, hipDeviceAttributeWallClockRate, dev) == hipSuccess && wclock > 0)
+        ticks_per_s = (double)wclock * 1000.0;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_icb = 0, o_clb = o_icb + up(4 * (size_t)(num_instances + 1));
+    const size_t o_lits = o_clb + up(4 * (size_t)(C + 1));
+    const size_t o_nv = o_lits + up(4 * (size_t)std::max(Ltot, 1));
+    const size_t o_st = o_nv + up(4 * (size_t)num_instances);
+    const size_t o_al = o_st + up(4 * (size_t)num_instances);
+    const size_t o_as = o_al + up(4 * (size_t)num_instances);
+    const size_t o_stats = o_as + up(4 * (size_t)num_instances * std::max(assign_stride, 1));
+    const size_t o_vi = o_stats + up(8 * (size_t)num_instances * SATMI_CDCL_NSTATS);
+    const size_t o_wc = o_vi + up(8 * (size_t)num_instances);
+    const size_t o_arena = o_wc + 256;
+    const size_t total = o_arena + (size_t)grid * (size_t)lay.bytes;
+    unsigned char *d = nullptr;
+    SATMI_HIP(hipMalloc(&d, total));
+    hipStream_t s = nullptr;
+    int rc = SATMI_OK;
+    do {
+        auto h2d = [&](size_t off, const void *src, size_t bytes) {
+            return bytes ? hipMemcpyAsync(d + off, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+        };
+        if (h2d(o_icb, h_inst_clause_begin, 4 * (size_t)(num_instances + 1)) != hipSuccess ||
+            h2d(o_clb, h_clause_lit_begin, 4 * (size_t)(C + 1)) != hipSuccess ||
+            h2d(o_lits, h_lits, 4 * (size_t)Ltot) != hipSuccess ||
+            h2d(o_nv, nv.data(), 4 * (size_t)num_instances) != hipSuccess ||
+            hipMemsetAsync(d + o_wc, 0, 24, s) != hipSuccess) {
+            rc = hip_fail(hipGetLastError(), "satmi_cdcl_batch_host: staging");
+            break;
+        }
+        CdclArgs A;
+        A.inst_clause_begin = (const int32_t *)(d + o_icb);
+        A.clause_lit_begin = (const int32_t *)(d + o_clb);
+        A.lits = (const int32_t *)(d + o_lits);
+        A.inst_nvars = (const int32_t *)(d + o_nv);
+        A.num_instances = num_instances;
+        A.max_iter = max_iter;
+        A.time_limit_ticks = time_limit_s > 0 ? (uint64_t)(time_limit_s * ticks_per_s) : 0;
+        A.status = (int32_t *)(d + o_st);
+        A.assign_len = (int32_t *)(d + o_al);
+        A.assign = (int32_t *)(d + o_as);
+        A.assign_stride = assign_stride;
+        A.stats = (int64_t *)(d + o_stats);
+        A.var_inc = (double *)(d + o_vi);
+        A.arena = d + o_arena;
+        A.lay = lay;
+        A.work_counter = (uint32_t *)(d + o_wc);
+        hipLaunchKernelGGL(cdcl_kernel, dim3(grid), dim3(64), 0, s, A);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpy(h_status, d + o_st, 4 * (size_t)num_instances, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(h_assign_len, d + o_al, 4 * (size_t)num_instances, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && assign_stride > 0)
+            e = hipMemcpy(h_assign, d + o_as, 4 * (size_t)num_instances * assign_stride, hipMemcpyDeviceToHost);
+        if (e == hipSuccess)
+            e = hipMemcpy(h_stats, d + o_stats, 8 * (size_t)num_instances * SATMI_CDCL_NSTATS, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(h_var_inc, d + o_vi, 8 * (size_t)num_instances, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = hip_fail(e, "satmi_cdcl_batch_host: launch / copy back");
+    } while (0);
+    (void)hipFree(d);
+    return rc;
+}

@@ -245,65 +245,84 @@ __global__ void __launch_bounds__(256) dp_subsume_kernel(ClauseList L, const int
 }
 
 // The same filter for K <= 8 words per clause (<= 256 variables), one LANE per
-// new clause with its key in registers: a workgroup stages 256 candidate
-// subsets at a time in LDS (remaining clauses, then earlier new clauses) and
-// every lane tests its clause against each staged key -- all lanes read the same
-// LDS address (a broadcast, no bank conflicts), so one key load serves 256
-// tests and the candidate lists are read once per workgroup instead of once
-// per new clause.  The workgroup stops when all its lanes found a subset.
-// tests_out: subset tests performed (roofline input).
-constexpr int SUB_TILE = 256;
+// new clause with its key in registers.  Candidates are numbered c = 0 ..
+// nrem + m: remaining clauses first, then new clauses (new clause e is a
+// candidate of k only when e < k).  Block (x, y) tests the new clauses
+// sel[256x .. 256x + 256) (sel == nullptr: k = 256x + lane) against candidates
+// [c_lo + y*SUB_CHUNK, +SUB_CHUNK) below c_hi, staging 256 candidate keys at a
+// time in LDS: every lane reads the same LDS address (a broadcast, no bank
+// conflicts), so one key load serves 256 tests and a candidate is read once per
+// block.  A hit clears kept[k] (all ones before the first pass); a lane also
+// stops once another block cleared its clause, the block once all lanes stopped.
+// The host runs it twice: a short prefix of the candidates for every new clause
+// (most are subsumed early), then the rest for the survivors only, so the
+// long scans run on full waves.  tests_out: subset tests performed.
+constexpr int SUB_TILE = 256, SUB_CHUNK = 4096, SUB_PREFIX = 1024;
 template <int K>
 __global__ void __launch_bounds__(SUB_TILE) dp_subsume_tiled_kernel(ClauseList L, const int64_t *rlist, int64_t nrem,
                                                                     const uint64_t *rbits, const int64_t *ntlist,
-                                                                    int64_t m, int64_t *kept,
+                                                                    const int64_t *sel, int64_t nsel, int64_t c_lo,
+                                                                    int64_t c_hi, int64_t *kept,
                                                                     unsigned long long *tests_out) {
     __shared__ uint64_t tile[SUB_TILE][K];
+    __shared__ unsigned long long tsum;
+    __shared__ int64_t kmax_s;
     const int tid = threadIdx.x;
-    const int64_t k = (int64_t)blockIdx.x * SUB_TILE + tid;
-    const bool valid = k < m;
+    const int64_t s = (int64_t)blockIdx.x * SUB_TILE + tid;
+    const bool valid = s < nsel;
+    const int64_t k = valid ? (sel ? sel[s] : s) : 0;
+    if (tid == 0) {
+        tsum = 0;
+        kmax_s = 0;
+    }
+    __syncthreads();
+    if (valid) atomicMax((unsigned long long *)&kmax_s, (unsigned long long)k);
+    __syncthreads();
+    const int64_t c_beg = c_lo + (int64_t)blockIdx.y * SUB_CHUNK;
+    const int64_t c_end = min(min(c_beg + SUB_CHUNK, c_hi), nrem + kmax_s);   // no candidate beyond the last clause's
+    if (c_beg >= c_end) return;                                               // (block-uniform)
     uint64_t x[K];
 #pragma unroll
     for (int w = 0; w < K; ++w) x[w] = valid ? rbits[ntlist[k] * K + w] : 0ull;
-    bool alive = valid;
+    const int64_t mine = valid ? nrem + k : 0;   // candidates of clause k: c < nrem + k
+    bool alive = valid && c_beg < mine;
     uint64_t tests = 0;
-    const int64_t kmax = min(m, (int64_t)(blockIdx.x + 1) * SUB_TILE) - 1;   // the block's last new clause
-    // pass 0: remaining clauses (all of them); pass 1: new clauses before k
-    for (int pass = 0; pass < 2; ++pass) {
-        const int64_t n = pass == 0 ? nrem : kmax;
-        for (int64_t e0 = 0; e0 < n; e0 += SUB_TILE) {
-            if (!__syncthreads_or(alive)) break;
-            const int64_t e = e0 + tid;
-            if (e < n) {
-                const uint64_t *src = pass == 0 ? L.bits + rlist[e] * K : rbits + ntlist[e] * K;
+    for (int64_t e0 = c_beg; e0 < c_end; e0 += SUB_TILE) {
+        if (alive && __hip_atomic_load(&kept[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) alive = false;
+        if (!__syncthreads_or(alive)) break;
+        const int64_t e = e0 + tid;
+        if (e < c_end) {
+            const uint64_t *src = e < nrem ? L.bits + rlist[e] * K : rbits + ntlist[e - nrem] * K;
 #pragma unroll
-                for (int w = 0; w < K; ++w) tile[tid][w] = src[w];
-            }
-            __syncthreads();
-            const int cnt = (int)min((int64_t)SUB_TILE, (pass == 0 ? n : k) - e0);
-            if (alive) {
-                for (int j = 0; j < cnt; ++j) {
-                    uint64_t out = 0;
+            for (int w = 0; w < K; ++w) tile[tid][w] = src[w];
+        }
+        __syncthreads();
+        if (alive) {
+            const int cnt = (int)(min(min(e0 + SUB_TILE, c_end), mine) - e0);
+            for (int j = 0; j < cnt; ++j) {
+                uint64_t out = 0;
 #pragma unroll
-                    for (int w = 0; w < K; ++w) out |= tile[j][w] & ~x[w];
-                    ++tests;
-                    if (out == 0ull) {
-                        alive = false;
-                        break;
-                    }
+                for (int w = 0; w < K; ++w) out |= tile[j][w] & ~x[w];
+                ++tests;
+                if (out == 0ull) {
+                    alive = false;
+                    __hip_atomic_store(&kept[k], (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
                 }
             }
-            __syncthreads();
+            if (alive && e0 + SUB_TILE >= mine) alive = false;   // this lane's candidates are done
         }
+        __syncthreads();
     }
-    if (valid) kept[k] = alive;
-    // one atomic per workgroup
-    __shared__ unsigned long long tsum;
-    if (tid == 0) tsum = 0;
-    __syncthreads();
+    // one atomic per block
     atomicAdd(&tsum, (unsigned long long)tests);
     __syncthreads();
     if (tid == 0) atomicAdd(tests_out, tsum);
+}
+
+__global__ void dp_ones_kernel(int64_t *a, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        a[i] = 1;
 }
 
 // kept resolvent images: (pc - {var}) | (nc - {-var})  (REF.py:114)
@@ -641,23 +660,41 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         int64_t nkept = 0;
         if (m > 0) {
             DP_TRY(kept.need(8 * (size_t)m));
-            const int nb = (int)((m + SUB_TILE - 1) / SUB_TILE);
             const int64_t *rl = rlist.as<int64_t>(), *ntl = ntlist.as<int64_t>();
             const uint64_t *rb = rbits.as<uint64_t>();
             int64_t *kp = kept.as<int64_t>();
             unsigned long long *tc = (unsigned long long *)(misc.as<char>() + 40);
             SATMI_HIP(hipEventRecord(ev_sub[0], s));
-            if (K == 2)
-                hipLaunchKernelGGL((dp_subsume_tiled_kernel<2>), dim3(nb), dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl, m, kp, tc);
-            else if (K == 4)
-                hipLaunchKernelGGL((dp_subsume_tiled_kernel<4>), dim3(nb), dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl, m, kp, tc);
-            else if (K == 6)
-                hipLaunchKernelGGL((dp_subsume_tiled_kernel<6>), dim3(nb), dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl, m, kp, tc);
-            else if (K == 8)
-                hipLaunchKernelGGL((dp_subsume_tiled_kernel<8>), dim3(nb), dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl, m, kp, tc);
-            else
+            if (K <= 8 && (K & 1) == 0) {
+                auto tiled = [&](const int64_t *sel, int64_t nsel, int64_t lo, int64_t hi) {
+                    const dim3 g((unsigned)((nsel + SUB_TILE - 1) / SUB_TILE),
+                                 (unsigned)std::max<int64_t>(1, (hi - lo + SUB_CHUNK - 1) / SUB_CHUNK));
+                    if (K == 2)
+                        hipLaunchKernelGGL((dp_subsume_tiled_kernel<2>), g, dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl,
+                                           sel, nsel, lo, hi, kp, tc);
+                    else if (K == 4)
+                        hipLaunchKernelGGL((dp_subsume_tiled_kernel<4>), g, dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl,
+                                           sel, nsel, lo, hi, kp, tc);
+                    else if (K == 6)
+                        hipLaunchKernelGGL((dp_subsume_tiled_kernel<6>), g, dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl,
+                                           sel, nsel, lo, hi, kp, tc);
+                    else
+                        hipLaunchKernelGGL((dp_subsume_tiled_kernel<8>), g, dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl,
+                                           sel, nsel, lo, hi, kp, tc);
+                };
+                hipLaunchKernelGGL(dp_ones_kernel, dim3(grid_for(m)), dim3(PRIM_BLOCK), 0, s, kp, m);
+                const int64_t total = nr + m;
+                const int64_t pre = std::min<int64_t>(SUB_PREFIX, total);
+                tiled(nullptr, m, 0, pre);   // every new clause: the first candidates
+                if (pre < total) {           // survivors: the rest
+                    int64_t nsurv = 0;
+                    DP_TRY(compact(kp, m, kpos, tiles, grand, klist, &nsurv, s));
+                    if (nsurv > 0) tiled(klist.as<int64_t>(), nsurv, pre, total);
+                }
+            } else {
                 hipLaunchKernelGGL(dp_subsume_kernel, dim3(grid_for(m * 64)), dim3(PRIM_BLOCK), 0, s, Lc, rl, nr, rb,
                                    ntl, m, K, kp);
+            }
             SATMI_HIP(hipEventRecord(ev_sub[1], s));
             SATMI_HIP(hipGetLastError());
             SATMI_HIP(hipEventSynchronize(ev_sub[1]));

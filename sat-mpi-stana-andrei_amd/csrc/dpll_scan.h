@@ -8,7 +8,7 @@
 
 namespace satmi {
 
-constexpr int SPLIT_HELPERS_PER_CU = 4;
+constexpr int SPLIT_HELPERS_PER_CU = 1;   // measured: 1 best with two pipelined streams (4: -6 %, 8: -48 % at the N=8 share)
 
 struct ScanLaunch {
     int num_instances;

@@ -30,6 +30,7 @@ EXPORTED = (
     "satmi_dp_host", "satmi_dpll_scan_lds_bytes", "satmi_dpll_set_kernel", "satmi_dpll_plan",
     "satmi_dpll_launch_span", "satmi_wallclock_hz", "satmi_resolution_debug_slot_base",
     "satmi_resolution_last_stats", "satmi_dpll_set_split", "satmi_dpll_split_stats", "satmi_dp_last_stats",
+    "satmi_cdcl_batch_host",
 )
 
 
@@ -108,6 +109,9 @@ def load():
         i32p, i32p, i64p, ctypes.c_int, i32p, ctypes.c_int64, i64p, ctypes.c_int64, i64p, ctypes.c_int]
     L.satmi_resolution_debug_slot_base.argtypes = [ctypes.c_int64]
     L.satmi_dp_last_stats.argtypes = [i64p, i64p, i64p, i64p, P(ctypes.c_int), P(ctypes.c_double)]
+    L.satmi_cdcl_batch_host.argtypes = [ctypes.c_int, i32p, i32p, i32p, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_double, i32p, i32p, i32p, ctypes.c_int, i64p,
+                                        P(ctypes.c_double)]
     L.satmi_resolution_last_stats.argtypes = [i64p, i64p, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)]
     L.satmi_dp_host.argtypes = [

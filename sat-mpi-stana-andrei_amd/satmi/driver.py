@@ -24,16 +24,11 @@ import tracemalloc
 from . import solvers
 from .dp import DavisPutnamLimit
 from .resolution import ResolutionLimit
-from .solvers import (SolverTimeout, davis_putnam_solver, dpll_optimized, generate_large_formula, hybrid_solver,
-                      pysat_solver, resolution_solver)
+from .solvers import (SolverTimeout, cdcl_solve, davis_putnam_solver, dpll_optimized, generate_large_formula,
+                      hybrid_solver, pysat_solver, resolution_solver)
 
 TIMEOUT_SECONDS = 60
 _DEADLINE_ERRORS = (SolverTimeout, ResolutionLimit, DavisPutnamLimit)
-
-
-def cdcl_solve(formula):
-    """CDCLSolver (REF.py:217-384) is not on the MI355X path; the menu reports the call as an error."""
-    raise NotImplementedError("CDCL (REF.py:217-384) is not part of the MI355X solver path")
 
 
 SOLVERS = {

@@ -7,13 +7,14 @@ REF.py ("comparatie intre algoritmii de rezolvare a seturilor de clauze.py"):
     resolution_solver(formula) -> bool                                           REF.py:63-95
     davis_putnam_solver(formula) -> bool                                         REF.py:98-130
     dpll_optimized(formula, assignment=None) -> List[Assignment]                 REF.py:133-214
+    cdcl_solve(formula) -> Tuple[bool, Optional[Assignment]]                     REF.py:217-384
     hybrid_solver(formula, threshold=1000) -> List[Assignment]                   REF.py:400-404
     pysat_solver(formula) -> List[Assignment]                                    REF.py:387-397
 
 The solvers run on the MI355X through libsatmi.so; there is no CPU fallback.
 """
 import random
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 from . import _capi
 from .dpll import dpll_batch
@@ -111,6 +112,19 @@ def pysat_solver(formula: Formula) -> List[Assignment]:
         if solver.solve():
             return [{abs(lit): lit > 0 for lit in solver.get_model()}]
         return []
+
+
+def cdcl_solve(formula: Formula) -> Tuple[bool, Optional[Assignment]]:
+    """REF.py:382-384 on the GPU (csrc/cdcl.hip): the reference's CDCLSolver, same
+    watch-list / dict / activity orders, so the same verdict and the same model
+    dict.  The reference's loop can run forever; under the driver's deadline the
+    call raises SolverTimeout like the other solvers."""
+    from .cdcl import CdclLimit
+    from .cdcl import cdcl_solve as _gpu_cdcl
+    try:
+        return _gpu_cdcl(formula, time_limit=_time_limit)
+    except CdclLimit as e:
+        raise SolverTimeout(f"Timeout after {_time_limit:g} seconds" if _time_limit else str(e)) from e
 
 
 def hybrid_solver(formula: Formula, threshold=1000) -> List[Assignment]:

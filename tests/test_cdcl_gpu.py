@@ -1,0 +1,74 @@
+"""GPU parity of the CDCL kernel (csrc/cdcl.hip) through the C ABI: against the
+reference's own CDCLSolver (tests/golden/cdcl_ref.json) and the oracle
+(oracle/cdcl_oracle.c) -- verdict, the assignment dict in insertion order,
+var_inc bit for bit, decision level and the loop's counts."""
+import json
+import os
+import random
+
+import pytest
+
+import oracle
+from satmi.cdcl import CDCL_SAT, CDCL_UNSAT, CDCL_LIMIT, cdcl_batch
+
+pytestmark = pytest.mark.gpu
+
+STATUS = {1: CDCL_SAT, 0: CDCL_UNSAT, -1: CDCL_LIMIT}
+
+
+def _check(r, want_result, want_assign, want_var_inc, want_stats):
+    assert r["status"] == STATUS[want_result]
+    assert r["assignment"] == want_assign
+    assert r["var_inc"] == want_var_inc
+    for k, v in want_stats.items():
+        assert r["stats"][k] == v, k
+
+
+def test_cdcl_matches_reference_class(golden_dir):
+    with open(os.path.join(golden_dir, "cdcl_ref.json")) as fh:
+        cases = json.load(fh)["cases"]
+    by_cap = {}
+    for c in cases:
+        by_cap.setdefault(c["max_iter"], []).append(c)
+    for cap, cs in by_cap.items():
+        rs = cdcl_batch([c["formula"] for c in cs], max_iter=cap)
+        for r, c in zip(rs, cs):
+            want = {k: c["stats"][k] for k in ("iterations", "conflicts", "decisions", "learned")}
+            want.update(level=c["level"], clauses=c["clauses"], watch_keys=c["watch_keys"])
+            _check(r, c["result"], c["assignment"], c["var_inc"], want)
+
+
+@pytest.mark.parametrize("seed,count,nmax,kmax,cap", [(1, 200, 16, 4, 3000), (2, 64, 40, 6, 20000)])
+def test_cdcl_matches_oracle_random(seed, count, nmax, kmax, cap):
+    """Random formulas (repeated literals and tautologies included) on long
+    runs: the set tables resize, dummies recycle, var_inc drifts."""
+    rng = random.Random(seed)
+    fs = []
+    for _ in range(count):
+        n = rng.randint(2, nmax)
+        f = []
+        for _ in range(rng.randint(1, 5 * n)):
+            k = rng.randint(1, min(kmax, n))
+            c = [v if rng.random() < 0.5 else -v for v in rng.sample(range(1, n + 1), k)]
+            if rng.random() < 0.1:
+                c.append(c[0] if rng.random() < 0.5 else -c[0])
+            f.append(c)
+        fs.append(f)
+    rs = cdcl_batch(fs, max_iter=cap)
+    for f, r in zip(fs, rs):
+        o = oracle.cdcl(f, cap)
+        _check(r, o["result"], o["assignment"], o["var_inc"],
+               {k: o["stats"][k] for k in ("iterations", "conflicts", "decisions", "learned", "clauses",
+                                           "watch_keys", "level")})
+
+
+def test_cdcl_drop_in_and_driver_row():
+    from satmi import driver
+    from satmi.solvers import cdcl_solve
+    f = [[1, 2], [-1, 2], [-2, 3]]
+    o = oracle.cdcl(f)
+    sat, model = cdcl_solve([list(c) for c in f])
+    assert sat and list(model.items()) == [(abs(l), l > 0) for l in o["assignment"]]
+    # [[-1, -2]] loops forever in the reference (rezultat.txt's CDCL timeouts): a timeout row
+    results = driver.run_solvers([[-1, -2]], [("CDCL", cdcl_solve)], timeout=1, print_fn=lambda *a: None)
+    assert results["CDCL"]["output"] == "Timeout after 1 seconds"

@@ -64,8 +64,11 @@ def test_read_formula_from_input():
 
 
 def test_scripted_menu_session(tmp_path):
+    def failing(formula):
+        raise RuntimeError("boom")
+
     table = {"1": ("Resolution", lambda f: False), "3": ("DPLL", lambda f: [{1: True}]),
-             "4": ("CDCL", driver.cdcl_solve)}
+             "4": ("CDCL", failing)}
     feed = iter(["1", "1 0", "-1 0", "done", "7", "y", "2", "3"])
     printed = []
     report = tmp_path / "rezultat.txt"
@@ -73,5 +76,5 @@ def test_scripted_menu_session(tmp_path):
     text = report.read_text()
     assert "Resolution" in text and "Formula is unsatisfiable" in text
     assert "Found 1 solution(s)" in text
-    assert "CDCL            Error        " in text   # unimplemented solver is reported as an error row
+    assert "CDCL            Error        " in text   # a failing solver is reported as an error row
     assert printed[-1] == "Exiting program."

@@ -93,3 +93,22 @@ def test_sound_mode_matches_reference_rewritten_branch(golden_dir):
                 assert r["counters"][k] == c["full"]["counters"][k], (c["tag"], k, f)
             assert r["counters"]["solutions"] == c["full"]["solutions"]
             assert (r["solutions"][0] if r["solutions"] else None) == c["full"]["first_solution"]
+
+
+def test_cdcl_matches_reference_class(golden_dir):
+    """oracle/cdcl_oracle.c against the reference's own CDCLSolver
+    (tests/golden/cdcl_ref.json, make_golden_cdcl.py): verdict, the assignment
+    dict in insertion order, decision level, var_inc (bit-exact float64), formula
+    length, watch-list keys and the loop's counts -- also where the reference's
+    unbounded loop was stopped after max_iter iterations."""
+    cases = _load(golden_dir, "cdcl_ref.json")
+    assert len(cases) >= 150 and {c["result"] for c in cases} >= {0, 1, -1}
+    for c in cases:
+        r = oracle.cdcl(c["formula"], c["max_iter"])
+        assert r["result"] == c["result"], c["formula"]
+        assert r["assignment"] == c["assignment"], c["formula"]
+        assert r["var_inc"] == c["var_inc"]
+        assert r["stats"]["level"] == c["level"]
+        assert r["stats"]["clauses"] == c["clauses"] and r["stats"]["watch_keys"] == c["watch_keys"]
+        for k in ("iterations", "conflicts", "decisions", "learned"):
+            assert r["stats"][k] == c["stats"][k], (k, c["formula"])
