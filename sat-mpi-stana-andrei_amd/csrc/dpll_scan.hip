@@ -789,6 +789,11 @@ struct SplitCfg {
 constexpr int SPLIT_POOL_OFF = 512;
 static_assert(sizeof(SplitCfg) == SPLIT_POOL_OFF, "SplitCfg layout");
 constexpr uint32_t SPLIT_MASK = 15u;   // a donation check every 16 decisions
+constexpr int SPLIT_MAX_PER_WAVE = 8;   // split a launch only below this many instances per resident wave
+// Kernels come in two forms: SPLIT = false has no branch-splitting code at all
+// (its register cost -- SGPR spills in the node loop -- was measured at ~4 % of
+// the full-size rate), SPLIT = true can split.  The host launches the split
+// form only for launches with few instances per resident wave.
 enum : uint32_t { SL_PENDING = 1, SL_RUNNING = 2, SL_DONE = 3, SL_RECLAIMED = 4 };
 struct SlotFlags {     // line 0 of a slot
     uint32_t state;    // split_epoch << 4 | SL_*
@@ -954,8 +959,9 @@ __device__ void merge_counters(int64_t *ctr, Ctr32 &c, bool &flushed, const Slot
 // Search instance b from its root (task < 0: results into the instance's
 // rows), or the donated subtree of split slot `task` (results into the slot).
 // dst: this wave's donation stack.
-template <int K, bool INC, typename C>
+template <int K, bool INC, typename C, bool SPLIT>
 __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, int task, int32_t *dst) {
+    SplitCfg *const SPL = SPLIT ? A.split : nullptr;
     using W = typename Pack<K>::W;
     constexpr uint32_t DON = SLds<K, C>::PHASE_BIT;   // ftrail: the frame's False branch was donated
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -1035,7 +1041,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     uint32_t dchk = 0;             // decisions since the last donation check
     // the row's tick count collects helpers' busy time minus time spent waiting
     // on them; the wave's own elapsed time is added at the end
-    if (A.split && ln == 0) st_agent(&ctr[SATMI_CTR_TICKS], (int64_t)0);
+    if (SPL && ln == 0) st_agent(&ctr[SATMI_CTR_TICKS], (int64_t)0);
     if (!is_task) {
         // root snapshot: the input's unit clauses in order (no clause is empty yet)
         int root_empty = INT_MAX;   // no clause is empty before any assignment
@@ -1101,13 +1107,13 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                 ++c.nodes;                                     // recursive call; its unit_propagate is a no-op
             } else if (!leaf) {                                // REF.py:208-213, as formula + [[var]]
                 const uint32_t v = r.best_var;
-                if (A.split && ((++dchk & SPLIT_MASK) == 0u)) {
+                if (SPL && ((++dchk & SPLIT_MASK) == 0u)) {
                     if (is_task && uniform_u32(ld_agent(&slot_ref(A, task).f->cancel))) {
                         status = SATMI_DPLL_TIMEOUT;           // abandoned: the donor found its model first
                         state = ST_DONE;
                         continue;
                     }
-                    if (uniform_i32(ld_agent(&A.split->want)) > 0) try_donate<K>(A, S, depth, b, dst, nd);
+                    if (uniform_i32(ld_agent(&SPL->want)) > 0) try_donate<K>(A, S, depth, b, dst, nd);
                 }
                 ep = next_decision_epoch<K>(S, n, ep);
                 if (ln == 0) {
@@ -1239,7 +1245,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     } else if (ln == 0) {
         A.status[b] = status;
         ctr[SATMI_CTR_SOLUTIONS] = sols;
-        if (A.split) add_agent(&ctr[SATMI_CTR_TICKS], ticks);
+        if (SPL) add_agent(&ctr[SATMI_CTR_TICKS], ticks);
         else ctr[SATMI_CTR_TICKS] = ticks;
     }
 }
@@ -1283,8 +1289,9 @@ __device__ __forceinline__ int2 next_donation(SplitCfg *cfg, int num_instances) 
 // One wave's share of a launch: instances from the queue, then (splitting on)
 // donated subtrees until every instance of the launch has finished.  One call
 // site of solve_instance (one inlined copy: register pressure).
-template <int K, bool INC, typename C>
+template <int K, bool INC, typename C, bool SPLIT>
 __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) {
+    SplitCfg *const SPL = SPLIT ? A.split : nullptr;
     const int ln = lane_id();
     bool draining = false;   // the instance queue is empty: take donated subtrees
     for (;;) {
@@ -1296,24 +1303,24 @@ __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) 
             if (x < (uint32_t)A.num_instances) {
                 b = (int)x;
             } else {
-                if (!A.split) break;
+                if (!SPL) break;
                 // a bounded set of helpers stays; the rest free their slots
                 int h = 0;
-                if (ln == 0) h = add_agent(&A.split->helpers, 1);
-                if (uniform_i32(h) >= A.split->max_helpers) break;
+                if (ln == 0) h = add_agent(&SPL->helpers, 1);
+                if (uniform_i32(h) >= SPL->max_helpers) break;
                 draining = true;
-                if (ln == 0) add_agent(&A.split->want, 1);
+                if (ln == 0) add_agent(&SPL->want, 1);
             }
         }
         if (draining) {
-            const int2 w = next_donation(A.split, A.num_instances);
+            const int2 w = next_donation(SPL, A.num_instances);
             if (w.y < 0) break;
             b = w.x;
             task = w.y;
         }
         // wave-uniform (a divergent-looking b costs 64-bit VGPR address math)
-        solve_instance<K, INC, C>(A, S, uniform_i32(b), uniform_i32(task), dst);
-        if (A.split && ln == 0) add_agent(task < 0 ? (int32_t *)&A.split->done : &A.split->want, 1);
+        solve_instance<K, INC, C, SPLIT>(A, S, uniform_i32(b), uniform_i32(task), dst);
+        if (SPL && ln == 0) add_agent(task < 0 ? (int32_t *)&SPL->done : &SPL->want, 1);
         wave_sync();
     }
 }
@@ -1325,7 +1332,7 @@ __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) 
 // addresses lv[code] with the code register and an immediate offset (no
 // per-wave base add per literal).  LVS = 0: multi-wave workgroups, the waves
 // taking consecutive images of the dynamic LDS, lv included.
-template <int K, int LVS, bool INC>
+template <int K, int LVS, bool INC, bool SPLIT>
 __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpll_scan_kernel(ScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     using C = std::conditional_t<LVS == 256, uint8_t, uint16_t>;
@@ -1356,7 +1363,7 @@ __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpl
     }
     span_begin(A.work_counter);
     const size_t wave_gid = (size_t)blockIdx.x * (blockDim.x >> 6) + (size_t)wave;
-    run_queue<K, INC, C>(A, S, A.split ? split_dstack(A.split, wave_gid) : nullptr);
+    run_queue<K, INC, C, SPLIT>(A, S, SPLIT ? split_dstack(A.split, wave_gid) : nullptr);
     span_end(A.work_counter);
 }
 
@@ -1366,7 +1373,7 @@ __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpl
 // to keep live or add (the runtime-layout kernel spends an SGPR and a VALU
 // add per access).  5,108 B of LDS per wave at FIXM = 448: 32 waves per CU.
 constexpr int FIX_NCAP = 127;
-template <int FIXM>
+template <int FIXM, bool SPLIT>
 __global__ void __launch_bounds__(64, SATMI_SCAN_WAVES_PER_SIMD) dpll_fixed_kernel(ScanArgs A) {
     static_assert(FIXM % 64 == 0, "whole 64-clause chunks");
     __shared__ __attribute__((aligned(16))) uint32_t cls_s[FIXM];
@@ -1396,7 +1403,7 @@ __global__ void __launch_bounds__(64, SATMI_SCAN_WAVES_PER_SIMD) dpll_fixed_kern
     for (int w = lane_id(); w < FIXM / 32; w += 64) S.bm[w].x = 0u;
     wave_sync();
     span_begin(A.work_counter);
-    run_queue<3, true, uint8_t>(A, S, A.split ? split_dstack(A.split, blockIdx.x) : nullptr);
+    run_queue<3, true, uint8_t, SPLIT>(A, S, SPLIT ? split_dstack(A.split, blockIdx.x) : nullptr);
     span_end(A.work_counter);
 }
 constexpr int FIX_MCAP = 448;   // configs[1] (n=50, m=213) and configs[2] (n=100, m=426)
@@ -1446,13 +1453,13 @@ bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, bool inc, u
 }
 
 template <bool INC>
-const void *scan_fn(int K, int lvs) {
+const void *scan_fn(int K, int lvs) {   // occupancy queries: the split form (the larger register budget)
     if (K == 3) {
-        if (lvs == 256) return (const void *)dpll_scan_kernel<3, 256, INC>;
-        if (lvs == 1024) return (const void *)dpll_scan_kernel<3, 1024, INC>;
-        return (const void *)dpll_scan_kernel<3, 0, INC>;
+        if (lvs == 256) return (const void *)dpll_scan_kernel<3, 256, INC, true>;
+        if (lvs == 1024) return (const void *)dpll_scan_kernel<3, 1024, INC, true>;
+        return (const void *)dpll_scan_kernel<3, 0, INC, true>;
     }
-    return lvs ? (const void *)dpll_scan_kernel<5, 4096, INC> : (const void *)dpll_scan_kernel<5, 0, INC>;
+    return lvs ? (const void *)dpll_scan_kernel<5, 4096, INC, true> : (const void *)dpll_scan_kernel<5, 0, INC, true>;
 }
 const void *scan_fn(int K, int lvs, bool inc) { return inc ? scan_fn<true>(K, lvs) : scan_fn<false>(K, lvs); }
 
@@ -1472,7 +1479,7 @@ bool fixed_class(int K, int max_vars, int max_clauses, bool inc) {
 // cheaper gather addressing) whenever they reach the same residency.
 int scan_plan(int K, int max_vars, int max_clauses, bool inc, ScanPlan *P) {
     if (fixed_class(K, max_vars, max_clauses, inc)) {
-        const void *fn = (const void *)dpll_fixed_kernel<FIX_MCAP>;
+        const void *fn = (const void *)dpll_fixed_kernel<FIX_MCAP, true>;
         int occ = 0, wgs = 32;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64, 0) == hipSuccess && occ > 0)
             wgs = std::min(wgs, occ);
@@ -1518,18 +1525,18 @@ int scan_plan(int K, int max_vars, int max_clauses, bool inc, ScanPlan *P) {
     return SATMI_OK;
 }
 
-template <bool INC>
+template <bool INC, bool SPLIT>
 void launch_kernel(int K, int lvs, dim3 g, dim3 blk, uint32_t wg_lds, hipStream_t s, const ScanArgs &A) {
     if (K == 3 && lvs == 256)
-        hipLaunchKernelGGL((dpll_scan_kernel<3, 256, INC>), g, blk, wg_lds, s, A);
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 256, INC, SPLIT>), g, blk, wg_lds, s, A);
     else if (K == 3 && lvs == 1024)
-        hipLaunchKernelGGL((dpll_scan_kernel<3, 1024, INC>), g, blk, wg_lds, s, A);
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 1024, INC, SPLIT>), g, blk, wg_lds, s, A);
     else if (K == 3)
-        hipLaunchKernelGGL((dpll_scan_kernel<3, 0, INC>), g, blk, wg_lds, s, A);
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 0, INC, SPLIT>), g, blk, wg_lds, s, A);
     else if (lvs)
-        hipLaunchKernelGGL((dpll_scan_kernel<5, 4096, INC>), g, blk, wg_lds, s, A);
+        hipLaunchKernelGGL((dpll_scan_kernel<5, 4096, INC, SPLIT>), g, blk, wg_lds, s, A);
     else
-        hipLaunchKernelGGL((dpll_scan_kernel<5, 0, INC>), g, blk, wg_lds, s, A);
+        hipLaunchKernelGGL((dpll_scan_kernel<5, 0, INC, SPLIT>), g, blk, wg_lds, s, A);
 }
 
 }  // namespace
@@ -1605,7 +1612,11 @@ int dpll_scan_launch(const ScanLaunch &L) {
     A.occ_cap = 0;
     A.lay = lay;
     A.split = nullptr;
-    if (L.split && L.split_alloc) {
+    // split only where the launch's tail matters: fewer than SPLIT_MAX_PER_WAVE
+    // instances per resident wave (at 32 per wave the tail is a few percent and
+    // the two-stream pipeline hides it; the split form's register cost is not)
+    const bool few = (int64_t)L.num_instances < (int64_t)SPLIT_MAX_PER_WAVE * grid * waves_per_wg;
+    if (L.split && L.split_alloc && few) {
         // slot pool: trail codes of the launch's entry width; one donation-stack
         // entry per decision frame per resident wave
         SplitCfg cfg{};
@@ -1639,9 +1650,13 @@ int dpll_scan_launch(const ScanLaunch &L) {
         }
     }
     const dim3 g(grid), blk(64 * waves_per_wg);
-    if (P.fixed) hipLaunchKernelGGL((dpll_fixed_kernel<FIX_MCAP>), g, blk, 0, L.stream, A);
-    else if (L.inc) launch_kernel<true>(K, P.lvs, g, blk, wg_lds, L.stream, A);
-    else launch_kernel<false>(K, P.lvs, g, blk, wg_lds, L.stream, A);
+    const bool sp = A.split != nullptr;
+    if (P.fixed && sp) hipLaunchKernelGGL((dpll_fixed_kernel<FIX_MCAP, true>), g, blk, 0, L.stream, A);
+    else if (P.fixed) hipLaunchKernelGGL((dpll_fixed_kernel<FIX_MCAP, false>), g, blk, 0, L.stream, A);
+    else if (L.inc && sp) launch_kernel<true, true>(K, P.lvs, g, blk, wg_lds, L.stream, A);
+    else if (L.inc) launch_kernel<true, false>(K, P.lvs, g, blk, wg_lds, L.stream, A);
+    else if (sp) launch_kernel<false, true>(K, P.lvs, g, blk, wg_lds, L.stream, A);
+    else launch_kernel<false, false>(K, P.lvs, g, blk, wg_lds, L.stream, A);
     SATMI_HIP(hipGetLastError());
     return SATMI_OK;
 }

@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsatmi.so")
+LIB_PATH = os.path.join(_HERE, os.environ.get("SATMI_LIB_VARIANT", "libsatmi.so"))   # A/B builds: libsatmi_*.so
 
 # include/satmi.h constants
 OK = 0
