@@ -325,8 +325,9 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
         const int total = lane63(incl);
         if (total <= 64) {
             // one touched clause per lane
-            int d = 0;
-            for (int b = 0; b < tl - rs; ++b) {
+            int d = __builtin_amdgcn_readlane(delta, 0);
+            if (tl - rs > 1)   // one batch literal: lane 0's list is the whole range
+            for (int b = 1; b < tl - rs; ++b) {
                 const int eb = __builtin_amdgcn_readlane(excl, b);
                 const int db = __builtin_amdgcn_readlane(delta, b);
                 d = ln >= eb ? db : d;
@@ -353,14 +354,18 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             if (nun <= FAST_UNITS) {
                 // a clause reached from two batch literals is one snapshot entry
                 bool dup = false;
-                for (uint64_t r = um; r; r &= r - 1) {
-                    const int u = __builtin_ctzll(r);
-                    dup |= u < ln && (uint32_t)__builtin_amdgcn_readlane((int)c, u) == c;
-                }
-                const uint64_t dm = __ballot(unit && !dup);
+                uint64_t dm = um;
                 int rank = 0;
-                for (uint64_t r = dm; r; r &= r - 1)
-                    rank += (uint32_t)__builtin_amdgcn_readlane((int)c, __builtin_ctzll(r)) < c ? 1 : 0;
+                if (nun > 1) {   // one unit: no duplicate, snapshot index 0
+                    for (uint64_t r = um; r; r &= r - 1) {
+                        const int u = __builtin_ctzll(r);
+                        const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)c, u);
+                        dup |= (u < ln) & (cu == c);   // no short circuit: no exec-mask branch
+                    }
+                    dm = __ballot(unit && !dup);
+                    for (uint64_t r = dm; r; r &= r - 1)
+                        rank += (uint32_t)__builtin_amdgcn_readlane((int)c, __builtin_ctzll(r)) < c ? 1 : 0;
+                }
                 if (unit && !dup) {
                     const uint32_t code = unit_code<K>(w, x);
                     S.snap[rank] = (C)code;
@@ -580,17 +585,16 @@ __device__ Choice choose(const SLds<K, C> &S, int n) {
     const uint64_t lt = lanemask_lt();
     int npure = 0;
     uint32_t maxc = 0;
+    // predicated (no exec-mask branches): lanes past n read variable n's words
     for (int v0 = 1; v0 <= n; v0 += 64) {
         const int v = v0 + ln;
-        bool pure = false;
-        uint32_t f = NONE32;
-        if (v <= n && var_free(S.lv, (uint32_t)v)) {
-            const uint32_t c = S.cnt[v];
-            const uint32_t p = c & 0xFFFFu, q = c >> 16;
-            maxc = max(maxc, p + q);
-            pure = (p + q) != 0u && (p == 0u || q == 0u);
-            f = S.first[v];
-        }
+        const uint32_t vc = (uint32_t)min(v, n);
+        const bool live = (v <= n) & var_free(S.lv, vc);
+        const uint32_t c = S.cnt[vc];
+        const uint32_t p = c & 0xFFFFu, q = c >> 16;
+        maxc = live ? max(maxc, p + q) : maxc;
+        const bool pure = live & ((p + q) != 0u) & ((p == 0u) | (q == 0u));
+        const uint32_t f = S.first[vc];
         const uint64_t mk = __ballot(pure);
         if (pure) S.plist[npure + __popcll(mk & lt)] = f;
         npure += __popcll(mk);
@@ -601,10 +605,11 @@ __device__ Choice choose(const SLds<K, C> &S, int n) {
         uint32_t bestf = NONE32;
         for (int v0 = 1; v0 <= n; v0 += 64) {
             const int v = v0 + ln;
-            if (v <= n && var_free(S.lv, (uint32_t)v)) {
-                const uint32_t c = S.cnt[v];
-                if ((c & 0xFFFFu) + (c >> 16) == maxc) bestf = min(bestf, S.first[v]);
-            }
+            const uint32_t vc = (uint32_t)min(v, n);
+            const uint32_t c = S.cnt[vc];
+            const bool best_here = (v <= n) & var_free(S.lv, vc) & ((c & 0xFFFFu) + (c >> 16) == maxc);
+            const uint32_t fv = S.first[vc];
+            bestf = best_here ? min(bestf, fv) : bestf;
         }
         bestf = wave_min_u32(bestf);
         best = uniform_u32(field<K>(S.cls[bestf >> 3], (int)(bestf & 7u)) >> 1);
