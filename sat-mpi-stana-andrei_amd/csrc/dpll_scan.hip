@@ -313,12 +313,11 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
     const int ln = lane_id();
     if (tl - rs <= 64) {
         // lane b: the b-th batch literal's negation and its occurrence list
-        int ob = 0, len = 0;
-        if (ln < tl - rs) {
-            const uint32_t x = (uint32_t)S.trail[rs + ln] ^ 1u;
-            ob = S.occ_off[x];
-            len = (int)S.occ_off[x + 1] - ob;
-        }
+        // predicated (no exec-mask branch): lanes past the batch read entry rs
+        const bool inb = ln < tl - rs;
+        const uint32_t x = (uint32_t)S.trail[inb ? rs + ln : rs] ^ 1u;
+        const int o0 = S.occ_off[x], o1 = S.occ_off[x + 1];
+        const int ob = inb ? o0 : 0, len = inb ? o1 - o0 : 0;
         const int incl = wave_incl_scan(len);
         const int excl = incl - len;
         const int delta = ob - excl;
@@ -502,9 +501,9 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
         for (int k0 = 0; k0 < nu; k0 += 64) {
             const int k = k0 + ln;
             const bool valid = k < nu;
-            const uint32_t code = valid ? (uint32_t)S.snap[k] : 0u;
+            const uint32_t code = (uint32_t)S.snap[valid ? k : 0];   // predicated loads
             const uint32_t v = code >> 1;
-            const bool first = valid && S.ts[v] == stamp(bep, (uint32_t)k);
+            const bool first = valid & (S.ts[v] == stamp(bep, (uint32_t)k));
             const uint64_t mk = __ballot(first);
             if (first) {
                 S.trail[tl + __popcll(mk & lt)] = (C)code;
