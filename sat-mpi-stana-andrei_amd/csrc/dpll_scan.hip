@@ -296,8 +296,9 @@ __device__ __forceinline__ int emptier(const SLds<K, C> &S, typename Pack<K>::W 
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const uint32_t code = field<K>(w, j);
-        const uint32_t st = code > CODE_DUMMY ? S.ts[code >> 1] : 0u;
-        if ((st >> 16) == bep) tt = max(tt, (int)stamp_index(st));
+        const uint32_t ts = S.ts[code >> 1];   // predicated: padding codes read variable 0's word
+        const uint32_t st = code > CODE_DUMMY ? ts : 0u;
+        tt = (st >> 16) == bep ? max(tt, (int)stamp_index(st)) : tt;
     }
     return tt;
 }
@@ -342,7 +343,8 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const uint32_t nf = sum_nfree(s);
             const bool empty = open && nf == 0u;
             if (__builtin_expect(__ballot(empty) != 0ull, 0)) {
-                const int e = empty ? emptier<K>(S, w, bep) : INT_MAX;
+                const int et = emptier<K>(S, w, bep);   // every lane: no exec-mask branch
+                const int e = empty ? et : INT_MAX;
                 *empty_at = wave_min_i32(e);
                 return 0;
             }
