@@ -82,9 +82,14 @@ def parse():
     p.add_argument("--kernel", choices=("auto", "inc", "scan", "general"), default="auto",
                    help="DPLL kernel policy (satmi_dpll_set_kernel); auto = incremental clause kernel")
     p.add_argument("--no-split", action="store_true", help="disable branch splitting (satmi_dpll_set_split)")
+    p.add_argument("--split-always", action="store_true",
+                   help="split every eligible launch (default: 1 to 8 instances per resident wave)")
+    p.add_argument("--split-warmup", type=int, default=-1,
+                   help="decisions before a search may donate (satmi_dpll_set_split_warmup; -1 = default)")
     p.add_argument("--helpers-per-cu", type=int, default=0, help="branch-splitting helpers per CU (0 = library default)")
-    p.add_argument("--streams", type=int, default=2, choices=(1, 2, 3, 4),
-                   help="HIP streams (each with its own resident batch) the steps rotate over")
+    p.add_argument("--streams", type=int, default=None, choices=(1, 2, 3, 4),
+                   help="HIP streams (each with its own resident batch) the steps rotate over (default: 3 for "
+                        "3sat-n50, whose 4,096 short searches leave most CU slots idle for a launch's 2 ms, else 2)")
     a = p.parse_args()
     if a.workload in SATURATION:
         return a
@@ -328,8 +333,12 @@ def main():
     L = _capi.load()
     _capi.set_kernel({"auto": _capi.KERNEL_AUTO, "inc": _capi.KERNEL_INC, "scan": _capi.KERNEL_SCAN,
                       "general": _capi.KERNEL_GENERAL}[args.kernel])
-    _capi.set_split(not args.no_split, args.helpers_per_cu)
-    NS = args.streams
+    _capi.set_split(_capi.SPLIT_OFF if args.no_split else _capi.SPLIT_ALWAYS if args.split_always
+                    else _capi.SPLIT_AUTO, args.helpers_per_cu)
+    _capi.set_split_warmup(args.split_warmup)
+    # measured (one MI355X): 3sat-n50 3.83 M (2 streams) -> 5.40-5.48 M instances/s (3);
+    # configs[2] full size equal, the N=8 share 496 k -> 463 k; 4 streams no better than 2
+    NS = args.streams or (3 if args.workload == "3sat-n50" else 2)
 
     n, k = args.n, args.k
     b0, b1 = shard_range(args.total, world, rank)   # this rank's contiguous shard of the step's batch
@@ -487,7 +496,8 @@ def main():
         "roofline_issue": issue_roofline(args.workload, B, kernel_ms),
     }
     if not args.no_split:   # the last launch's branch-splitting statistics (satmi_dpll_split_stats)
-        out["branch_split"] = _capi.split_stats(streams[(args.steps - 1) % NS].cuda_stream)
+        st = _capi.split_stats(streams[(args.steps - 1) % NS].cuda_stream)
+        out["branch_split"] = st if st["done"] else None   # None: the launch did not split (auto policy)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and not args.profile_steps:
             host = cnf.CnfBatch(icb.cpu().numpy(), clb.cpu().numpy(), lits.cpu().numpy(), nv.cpu().numpy())

@@ -234,10 +234,18 @@ int satmi_dpll_set_kernel(int policy);
  * the unsplit search (branches a sequential search would not have visited are
  * cancelled and count nothing).  Applies to SOUND-mode launches with
  * max_solutions == 1, no node limit and no time limit.
+ *   enable          0 off; 1 auto (default): launches with at least one and
+ *                   fewer than 8 instances per resident wavefront; 2 every
+ *                   eligible launch
  *   helpers_per_cu  wavefronts per CU that stay as helpers once the queue
  *                   drains (0 = default 1); the others exit, freeing their CU
  *                   slots for a launch queued on another stream */
 int satmi_dpll_set_split(int enable, int helpers_per_cu);
+
+/* Decisions a search makes before it may donate a branch (process-wide;
+ * < 0 = default 256, 0 = from its first donation check).  Short searches never
+ * split: their subtrees cost a helper more to restage than to search. */
+int satmi_dpll_set_split_warmup(int decisions);
 
 /* Branch-splitting statistics of the last split launch on `stream` (waits for
  * the stream): out[0..6] = donations, helper tickets, subtrees run by helpers,

@@ -1016,6 +1016,7 @@ static std::vector<DeviceWork> g_work;
 static std::atomic<int> g_kernel_policy{SATMI_KERNEL_AUTO};
 static std::atomic<int> g_split_enable{1};
 static std::atomic<int> g_split_helpers{SPLIT_HELPERS_PER_CU};
+static std::atomic<int> g_split_warmup{SPLIT_WARMUP_DECISIONS};
 
 static int device_work(hipStream_t stream, DeviceWork **out, uint32_t **counter) {
     int dev = 0;
@@ -1171,8 +1172,17 @@ extern "C" int satmi_dpll_set_split(int enable, int helpers_per_cu) {
         set_error("satmi_dpll_set_split: helpers_per_cu must be in [0, 32]");
         return SATMI_ERR_ARG;
     }
-    g_split_enable.store(enable ? 1 : 0);
+    if (enable < 0 || enable > 2) {
+        set_error("satmi_dpll_set_split: enable must be 0 (off), 1 (auto) or 2 (always)");
+        return SATMI_ERR_ARG;
+    }
+    g_split_enable.store(enable);
     g_split_helpers.store(helpers_per_cu ? helpers_per_cu : SPLIT_HELPERS_PER_CU);
+    return SATMI_OK;
+}
+
+extern "C" int satmi_dpll_set_split_warmup(int decisions) {
+    g_split_warmup.store(decisions < 0 ? SPLIT_WARMUP_DECISIONS : decisions);
     return SATMI_OK;
 }
 
@@ -1311,8 +1321,11 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
         Lc.occ_alloc = [stream](size_t bytes) { return occ_scratch((hipStream_t)stream, bytes); };
         // branch splitting reproduces the sequential search exactly only when
         // the search stops at its first model and nothing else cuts it short
-        Lc.split = g_split_enable.load() && max_solutions == 1 && node_limit <= 0 && time_limit_s <= 0;
+        const int sm = g_split_enable.load();
+        Lc.split = sm && max_solutions == 1 && node_limit <= 0 && time_limit_s <= 0;
+        Lc.split_always = sm == 2;
         Lc.split_helpers_per_cu = g_split_helpers.load();
+        Lc.split_warmup = g_split_warmup.load();
         Lc.split_alloc = [stream](size_t bytes, uint32_t *epoch) {
             return split_scratch((hipStream_t)stream, bytes, epoch);
         };

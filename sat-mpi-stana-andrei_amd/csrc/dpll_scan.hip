@@ -790,7 +790,8 @@ struct SplitCfg {
     uint32_t epoch;            // launch tag of the slot states (the pool is not cleared between launches)
     int32_t max_helpers;       // waves beyond this count exit when the queue drains (their CU slots go
                                // to the next launch on another stream)
-    uint32_t pad3[27];
+    uint32_t warm;             // decisions of a search before it may donate
+    uint32_t pad3[26];
 };
 constexpr int SPLIT_POOL_OFF = 512;
 static_assert(sizeof(SplitCfg) == SPLIT_POOL_OFF, "SplitCfg layout");
@@ -1119,7 +1120,8 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                         state = ST_DONE;
                         continue;
                     }
-                    if (uniform_i32(ld_agent(&SPL->want)) > 0) try_donate<K>(A, S, depth, b, dst, nd);
+                    if (dchk >= SPL->warm && uniform_i32(ld_agent(&SPL->want)) > 0)
+                        try_donate<K>(A, S, depth, b, dst, nd);
                 }
                 ep = next_decision_epoch<K>(S, n, ep);
                 if (ln == 0) {
@@ -1620,8 +1622,13 @@ int dpll_scan_launch(const ScanLaunch &L) {
     A.split = nullptr;
     // split only where the launch's tail matters: fewer than SPLIT_MAX_PER_WAVE
     // instances per resident wave (at 32 per wave the tail is a few percent and
-    // the two-stream pipeline hides it; the split form's register cost is not)
-    const bool few = (int64_t)L.num_instances < (int64_t)SPLIT_MAX_PER_WAVE * grid * waves_per_wg;
+    // the two-stream pipeline hides it; the split form's register cost is not),
+    // but at least one per resident wave (a launch that leaves CU slots empty
+    // from the start -- configs[1]: 4,096 short searches -- loses 7 % to the
+    // split form and gains nothing: the other stream's launch fills those slots)
+    const int64_t waves = (int64_t)grid * waves_per_wg;
+    const bool few = L.split_always || ((int64_t)L.num_instances < (int64_t)SPLIT_MAX_PER_WAVE * waves &&
+                                        (int64_t)L.num_instances >= (int64_t)L.num_cus * P.wg_per_cu * waves_per_wg);
     if (L.split && L.split_alloc && few) {
         // slot pool: trail codes of the launch's entry width; one donation-stack
         // entry per decision frame per resident wave
@@ -1632,6 +1639,7 @@ int dpll_scan_launch(const ScanLaunch &L) {
         cfg.slot_cap = (int)std::min<size_t>(1u << 18, ((size_t)256 << 20) / (size_t)cfg.slot_bytes);
         cfg.dstack_cap = ncap + 1;
         cfg.max_helpers = L.num_cus * L.split_helpers_per_cu;
+        cfg.warm = (uint32_t)std::max(L.split_warmup, 0);
         const size_t pool = (size_t)cfg.slot_cap * (size_t)cfg.slot_bytes;
         const size_t stacks = (size_t)grid * (size_t)waves_per_wg * (size_t)cfg.dstack_cap * sizeof(int32_t);
         uint32_t epoch = 0;

@@ -30,7 +30,7 @@ EXPORTED = (
     "satmi_dp_host", "satmi_dpll_scan_lds_bytes", "satmi_dpll_set_kernel", "satmi_dpll_plan",
     "satmi_dpll_launch_span", "satmi_wallclock_hz", "satmi_resolution_debug_slot_base",
     "satmi_resolution_last_stats", "satmi_dpll_set_split", "satmi_dpll_split_stats", "satmi_dp_last_stats",
-    "satmi_cdcl_batch_host",
+    "satmi_cdcl_batch_host", "satmi_dpll_set_split_warmup",
 )
 
 
@@ -39,10 +39,19 @@ def set_kernel(policy):
     check(load().satmi_dpll_set_kernel(int(policy)), "satmi_dpll_set_kernel")
 
 
+SPLIT_OFF, SPLIT_AUTO, SPLIT_ALWAYS = 0, 1, 2
+
+
 def set_split(enable, helpers_per_cu=0):
-    """Process-wide branch splitting of the clause kernels' launch tails (default on;
-    helpers_per_cu 0 = the library default)."""
-    check(load().satmi_dpll_set_split(int(bool(enable)), int(helpers_per_cu)), "satmi_dpll_set_split")
+    """Process-wide branch splitting of the clause kernels' launch tails: False/SPLIT_OFF,
+    True/SPLIT_AUTO (default: launches with 1 to 8 instances per resident wave) or
+    SPLIT_ALWAYS; helpers_per_cu 0 = the library default."""
+    check(load().satmi_dpll_set_split(int(enable), int(helpers_per_cu)), "satmi_dpll_set_split")
+
+
+def set_split_warmup(decisions=-1):
+    """Decisions a search makes before it may donate a branch (-1 = the library default)."""
+    check(load().satmi_dpll_set_split_warmup(int(decisions)), "satmi_dpll_set_split_warmup")
 
 
 def split_stats(stream=None):
@@ -93,6 +102,7 @@ def load():
     L.satmi_dpll_set_kernel.argtypes = [ctypes.c_int]
     L.satmi_dpll_set_split.argtypes = [ctypes.c_int, ctypes.c_int]
     L.satmi_dpll_split_stats.argtypes = [vp, i64p]
+    L.satmi_dpll_set_split_warmup.argtypes = [ctypes.c_int]
     L.satmi_dpll_launch_span.argtypes = [vp, vp]
     L.satmi_wallclock_hz.argtypes = [P(ctypes.c_double)]
     L.satmi_dpll_plan.argtypes = [ctypes.c_int] * 6 + [P(ctypes.c_int), P(ctypes.c_uint64), P(ctypes.c_int)]

@@ -365,12 +365,16 @@ def test_scan_kernel_chunk_group_tails(n, m, cap):
         assert rs.solutions(b)[:1] == o["solutions"][:1]
 
 
-def _run_split(batch, split, policy=_capi.KERNEL_AUTO, **kw):
-    _capi.set_split(split)
+def _run_split(batch, split, policy=_capi.KERNEL_AUTO, warmup=0, **kw):
+    # warm-up 0: every search may donate from its first check (the protocol
+    # under the most stress; the default only splits long searches)
+    _capi.set_split(_capi.SPLIT_ALWAYS if split else _capi.SPLIT_OFF)
+    _capi.set_split_warmup(warmup)
     try:
         return _run_policy(batch, policy, **kw)
     finally:
         _capi.set_split(True)
+        _capi.set_split_warmup(-1)
 
 
 @pytest.mark.parametrize("n,m,B,policy", [(100, 426, 24, _capi.KERNEL_AUTO), (100, 426, 3000, _capi.KERNEL_AUTO),
