@@ -507,10 +507,12 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             const uint32_t v = code >> 1;
             const bool first = valid & (S.ts[v] == stamp(bep, (uint32_t)k));
             const uint64_t mk = __ballot(first);
-            if (first) {
-                S.trail[tl + __popcll(mk & lt)] = (C)code;
-                lv_assign(S.lv, code);
-            }
+            // predicated stores (no exec-mask branch): the other lanes write
+            // the first entry past the batch (dead: the trail is a stack, and
+            // tl + batch <= n <= ncap keeps it in the array) and re-assert the
+            // padding / dummy codes' fixed states
+            S.trail[tl + __popcll(mk & (first ? lt : ~0ull))] = (C)code;
+            lv_assign(S.lv, first ? code : CODE_DUMMY);
             tl += __popcll(mk);
         }
         wave_sync();
@@ -547,17 +549,17 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
 
 // literal_sign / var_counts scan (REF.py:174-179, :198-203): every free
 // occurrence in an active clause is counted per variable, and the first
-// position kept.  Returns the number of active clauses (0: REF.py:170-171).
+// position kept.  Returns whether any clause is active (none: REF.py:170-171).
 // Within an active clause the atomics run for every slot -- a falsified slot
 // adds 0 / mins NONE32, padding hits variable 0 (never read) -- so there is
 // no branch per slot.
 template <int K, typename C>
 __device__ int scan_counts(const SLds<K, C> &S, int mpad) {
     using W = typename Pack<K>::W;
-    int nact = 0;
+    uint64_t any = 0;   // only "no active clause" matters: OR the ballots (one scalar op per chunk)
     for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int c, W w, const uint32_t(&x)[K]) {
         const bool act = !sum_true(clause_sum<K>(x));
-        nact += __popcll(__ballot(act));
+        any |= __ballot(act);
         if (act) {
 #pragma unroll
             for (int j = 0; j < K; ++j) {
@@ -569,7 +571,7 @@ __device__ int scan_counts(const SLds<K, C> &S, int mpad) {
         }
     });
     wave_sync();
-    return nact;
+    return any != 0ull;
 }
 
 struct Choice {
