@@ -87,8 +87,8 @@ def parse():
     p.add_argument("--split-warmup", type=int, default=-1,
                    help="decisions before a search may donate (satmi_dpll_set_split_warmup; -1 = default)")
     p.add_argument("--helpers-per-cu", type=int, default=0, help="branch-splitting helpers per CU (0 = library default)")
-    p.add_argument("--streams", type=int, default=None, choices=range(1, 9),
-                   help="HIP streams (each with its own resident batch) the steps rotate over (default: 8 for "
+    p.add_argument("--streams", type=int, default=None, choices=range(1, 17),
+                   help="HIP streams (each with its own resident batch) the steps rotate over (default: 16 for "
                         "3sat-n50, whose 4,096 short searches leave most CU slots idle for a launch's 2 ms, else 2)")
     a = p.parse_args()
     if a.workload in SATURATION:
@@ -323,10 +323,10 @@ def main():
     if args.workload in SATURATION:
         return saturation_main(args)
     # measured (one MI355X, profiles/r02/final/streams.txt): 3sat-n50 3.83 M instances/s
-    # on 2 streams, 5.40 M on 3, 6.32 M on 4, 7.28 M on 8 (wave slots then over-subscribed:
-    # busy wave-time 1.13 x resident); configs[2] the same on 2, 3 or 4 streams, its N=8
-    # share 496 k on 2 and 4, 463 k on 3
-    NS = args.streams or (8 if args.workload == "3sat-n50" else 2)
+    # on 2 streams, 5.40 M on 3, 6.32 M on 4, 7.5 M on 8, 8.6 M on 12, 9.3 M on 16 (with
+    # --steps >= 8 x streams); configs[2] the same on 2, 3 or 4 streams, its N=8 share
+    # 496 k on 2 and 4, 463 k on 3
+    NS = args.streams or (16 if args.workload == "3sat-n50" else 2)
     if NS > 3 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < NS + 1:
         # one hardware queue per stream (+ the null stream's) so the launches run
         # concurrently; HIP reads this when the runtime starts, below
