@@ -357,7 +357,14 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 bool dup = false;
                 uint64_t dm = um;
                 int rank = 0;
-                if (nun > 1) {   // one unit: no duplicate, snapshot index 0
+                if (nun == 2) {   // the commonest case, without loops: lanes u0 < u1
+                    const int u0 = __builtin_ctzll(um), u1 = 63 - __builtin_clzll(um);
+                    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)c, u0);
+                    const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)c, u1);
+                    dup = (ln == u1) & (c0 == c1);
+                    dm = c0 == c1 ? 1ull << u0 : um;   // a duplicate keeps lane u0 only
+                    rank = ln == u0 ? (c1 < c0 ? 1 : 0) : (c0 < c1 ? 1 : 0);
+                } else if (nun > 1) {   // one unit: no duplicate, snapshot index 0
                     for (uint64_t r = um; r; r &= r - 1) {
                         const int u = __builtin_ctzll(r);
                         const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)c, u);
