@@ -85,3 +85,22 @@ def test_scan_kernel_eligibility_query():
         _capi.set_kernel(_capi.KERNEL_AUTO)
     with pytest.raises(_capi.SatmiError):
         _capi.set_kernel(7)
+
+
+def test_split_policy_arguments():
+    """satmi_dpll_set_split: 0 off / 1 auto / 2 always, helpers in [0, 32];
+    satmi_dpll_set_split_warmup: < 0 restores the default (host-side state only)."""
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("libsatmi.so not built")
+    try:
+        for mode in (_capi.SPLIT_OFF, _capi.SPLIT_ALWAYS, _capi.SPLIT_AUTO):
+            _capi.set_split(mode)
+        with pytest.raises(_capi.SatmiError):
+            _capi.set_split(3)
+        with pytest.raises(_capi.SatmiError):
+            _capi.set_split(_capi.SPLIT_AUTO, helpers_per_cu=33)
+        _capi.set_split_warmup(0)
+        _capi.set_split_warmup(1000)
+    finally:
+        _capi.set_split(_capi.SPLIT_AUTO)
+        _capi.set_split_warmup(-1)

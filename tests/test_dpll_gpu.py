@@ -164,6 +164,36 @@ def test_configs4_batch_properties(n, m, k, cap, B):
         assert r.counter_dict(b) == {**r.counter_dict(b), **{k_: o["counters"][k_] for k_ in CTR}}
 
 
+@pytest.mark.parametrize("split", [_capi.SPLIT_OFF, _capi.SPLIT_ALWAYS])
+def test_configs4_uf250_solved_to_completion(golden_dir, split):
+    """configs[4] uf250-shaped searches run to the end (no node cap; 10^5-10^6
+    calls each): status, every counter and the model equal the oracle's
+    (tests/golden/fullsolve_uf250.json, make_fullsolve.py), with and without
+    branch splitting (24 searches on thousands of idle waves: helpers take
+    subtrees of searches a million calls deep)."""
+    with open(os.path.join(golden_dir, "fullsolve_uf250.json")) as fh:
+        g = json.load(fh)
+    batch = cnf.uniform_ksat(g["count"], g["n"], g["m"], g["k"], seed=g["seed"])
+    import hashlib
+    assert hashlib.sha256(batch.lits.tobytes()).hexdigest() == g["lits_sha256"]
+    cases = g["cases"]
+    assert len(cases) >= 8
+    fs = [batch.instance(c["index"]) for c in cases]   # only the searches the oracle finished
+    _capi.set_split(split)
+    try:
+        r = dpll_batch(fs, mode="sound", max_solutions=1, sol_cap=1)   # a time limit would disable splitting
+    finally:
+        _capi.set_split(_capi.SPLIT_AUTO)
+    for b, c in enumerate(cases):
+        assert int(r.status[b]) == c["status"], c["index"]
+        got = r.counter_dict(b)
+        for key in CTR:
+            assert got[key] == c["counters"][key], (c["index"], key)
+        assert r.solutions(b)[:1] == ([c["model"]] if c["model"] else []), c["index"]
+        if c["model"]:
+            assert _satisfies(fs[b], c["model"])
+
+
 def _random_mix(seed, count, nmax, kmax, mmax):
     rng = random.Random(seed)
     fs = []

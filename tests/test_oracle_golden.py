@@ -112,3 +112,23 @@ def test_cdcl_matches_reference_class(golden_dir):
         assert r["stats"]["clauses"] == c["clauses"] and r["stats"]["watch_keys"] == c["watch_keys"]
         for k in ("iterations", "conflicts", "decisions", "learned"):
             assert r["stats"][k] == c["stats"][k], (k, c["formula"])
+
+
+def test_fullsolve_fixture_regenerates(golden_dir):
+    """tests/golden/fullsolve_uf250.json (make_fullsolve.py): the instances
+    regenerate bit-identically from their seed, and the oracle reproduces the
+    recorded searches that finish quickly (the long ones are the GPU test's)."""
+    import hashlib
+
+    from satmi import cnf
+    with open(os.path.join(golden_dir, "fullsolve_uf250.json")) as fh:
+        g = json.load(fh)
+    batch = cnf.uniform_ksat(g["count"], g["n"], g["m"], g["k"], seed=g["seed"])
+    assert hashlib.sha256(batch.lits.tobytes()).hexdigest() == g["lits_sha256"]
+    for c in g["cases"]:
+        if c["counters"]["nodes"] > 20000:
+            continue
+        o = oracle.dpll(batch.instance(c["index"]), "sound", max_solutions=1, sol_cap=1)
+        assert o["status"] == c["status"]
+        assert o["counters"] == c["counters"]
+        assert (o["solutions"][0] if o["solutions"] else []) == c["model"]
