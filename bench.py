@@ -85,7 +85,7 @@ def parse():
     p.add_argument("--split-always", action="store_true",
                    help="split every eligible launch (default: 1 to 8 instances per resident wave)")
     p.add_argument("--split-warmup", type=int, default=-1,
-                   help="decisions before a search may donate (satmi_dpll_set_split_warmup; -1 = default)")
+                   help="nodes before a search may donate (satmi_dpll_set_split_warmup; -1 = default)")
     p.add_argument("--helpers-per-cu", type=int, default=0, help="branch-splitting helpers per CU (0 = library default)")
     p.add_argument("--streams", type=int, default=None, choices=range(1, 17),
                    help="HIP streams (each with its own resident batch) the steps rotate over (default: 16 for "

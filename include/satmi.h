@@ -229,7 +229,7 @@ int satmi_dpll_set_kernel(int policy);
 /* Branch splitting in the clause kernels (process-wide; default on): once a
  * launch's instance queue drains, idle wavefronts take over the False branches
  * of open decisions of the searches still running (a search checks for idle
- * wavefronts every 16 decisions); the donor takes the helper's result when its
+ * wavefronts every 16 nodes); the donor takes the helper's result when its
  * backtracking reaches the branch.  Statuses, counters and models are those of
  * the unsplit search (branches a sequential search would not have visited are
  * cancelled and count nothing).  Applies to SOUND-mode launches with
@@ -242,10 +242,11 @@ int satmi_dpll_set_kernel(int policy);
  *                   slots for a launch queued on another stream */
 int satmi_dpll_set_split(int enable, int helpers_per_cu);
 
-/* Decisions a search makes before it may donate a branch (process-wide;
- * < 0 = default 256, 0 = from its first donation check).  Short searches never
- * split: their subtrees cost a helper more to restage than to search. */
-int satmi_dpll_set_split_warmup(int decisions);
+/* Nodes (recursive calls) a search visits before it may donate a branch
+ * (process-wide; < 0 = default 256, 0 = from its first donation check).  Short
+ * searches never split: their subtrees cost a helper more to restage than to
+ * search. */
+int satmi_dpll_set_split_warmup(int nodes);
 
 /* Branch-splitting statistics of the last split launch on `stream` (waits for
  * the stream): out[0..6] = donations, helper tickets, subtrees run by helpers,

@@ -1016,7 +1016,7 @@ static std::vector<DeviceWork> g_work;
 static std::atomic<int> g_kernel_policy{SATMI_KERNEL_AUTO};
 static std::atomic<int> g_split_enable{1};
 static std::atomic<int> g_split_helpers{SPLIT_HELPERS_PER_CU};
-static std::atomic<int> g_split_warmup{SPLIT_WARMUP_DECISIONS};
+static std::atomic<int> g_split_warmup{SPLIT_WARMUP_NODES};
 
 static int device_work(hipStream_t stream, DeviceWork **out, uint32_t **counter) {
     int dev = 0;
@@ -1181,8 +1181,8 @@ extern "C" int satmi_dpll_set_split(int enable, int helpers_per_cu) {
     return SATMI_OK;
 }
 
-extern "C" int satmi_dpll_set_split_warmup(int decisions) {
-    g_split_warmup.store(decisions < 0 ? SPLIT_WARMUP_DECISIONS : decisions);
+extern "C" int satmi_dpll_set_split_warmup(int nodes) {
+    g_split_warmup.store(nodes < 0 ? SPLIT_WARMUP_NODES : nodes);
     return SATMI_OK;
 }
 

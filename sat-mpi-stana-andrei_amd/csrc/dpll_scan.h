@@ -9,9 +9,9 @@
 namespace satmi {
 
 constexpr int SPLIT_HELPERS_PER_CU = 1;   // measured: 1 best with two pipelined streams (4: -6 %, 8: -48 % at the N=8 share)
-// decisions a search makes before it may donate: short searches (most of
+// nodes a search visits before it may donate: short searches (most of
 // configs[1]) would only ship overhead to the helpers
-constexpr int SPLIT_WARMUP_DECISIONS = 256;
+constexpr int SPLIT_WARMUP_NODES = 256;
 
 struct ScanLaunch {
     int num_instances;
@@ -37,7 +37,7 @@ struct ScanLaunch {
     bool split = false;
     bool split_always = false;   // split any eligible launch (else only 1 <= instances per resident wave < 8)
     int split_helpers_per_cu = SPLIT_HELPERS_PER_CU;   // waves per CU that stay as helpers once the queue drains
-    int split_warmup = SPLIT_WARMUP_DECISIONS;   // decisions of a search before its first donation
+    int split_warmup = SPLIT_WARMUP_NODES;   // nodes of a search before its first donation
     std::function<void *(size_t, uint32_t *)> split_alloc;
 };
 

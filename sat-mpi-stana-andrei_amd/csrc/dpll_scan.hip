@@ -782,7 +782,7 @@ __device__ uint64_t flush_counters(int64_t *ctr, Ctr32 &c, bool &flushed) {
 // Head of the splitting scratch, rewritten before each launch (the slot pool
 // follows at SPLIT_POOL_OFF, then the per-wave donation stacks).  One 128-B
 // line per access pattern: the queue line is polled by the helpers, the
-// request line read by every searching wave every SPLIT_MASK + 1 decisions --
+// request line read by every searching wave every SPLIT_CHECK_NODES nodes --
 // kept apart so that polling never queues the searches' reads.
 struct SplitCfg {
     uint32_t pub;              // line 0: slots allocated
@@ -799,12 +799,15 @@ struct SplitCfg {
     uint32_t epoch;            // launch tag of the slot states (the pool is not cleared between launches)
     int32_t max_helpers;       // waves beyond this count exit when the queue drains (their CU slots go
                                // to the next launch on another stream)
-    uint32_t warm;             // decisions of a search before it may donate
+    uint32_t warm;             // nodes of a search before it may donate
     uint32_t pad3[26];
 };
 constexpr int SPLIT_POOL_OFF = 512;
 static_assert(sizeof(SplitCfg) == SPLIT_POOL_OFF, "SplitCfg layout");
-constexpr uint32_t SPLIT_MASK = 15u;   // a donation check every 16 decisions
+// A donation check every SPLIT_CHECK_NODES nodes, run from the node loop's
+// existing event test (next_event), so the split form's loop carries no
+// per-decision counter: what it keeps live is only read at the checks.
+constexpr uint32_t SPLIT_CHECK_NODES = 16u;
 constexpr int SPLIT_MAX_PER_WAVE = 8;   // split a launch only below this many instances per resident wave
 // Kernels come in two forms: SPLIT = false has no branch-splitting code at all
 // (its register cost -- SGPR spills in the node loop -- was measured at ~4 % of
@@ -1046,7 +1049,8 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     int64_t sols = 0;
     bool flushed = false;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t next_event = next_event_after(A, 0);
+    uint32_t next_flush = next_event_after(A, 0);
+    uint32_t next_event = SPL ? min(next_flush, SPLIT_CHECK_NODES) : next_flush;
     int depth = 0, tl = 0;
     int status = SATMI_DPLL_EXHAUSTED;
     int state;
@@ -1054,7 +1058,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     int nu = 0;
     bool dec_round = false;
     int nd = 0;                    // live entries of the donation stack
-    uint32_t dchk = 0;             // decisions since the last donation check
+    uint32_t nchk = 0;             // donation checks so far
     // the row's tick count collects helpers' busy time minus time spent waiting
     // on them; the wave's own elapsed time is added at the end
     if (SPL && ln == 0) st_agent(&ctr[SATMI_CTR_TICKS], (int64_t)0);
@@ -1123,15 +1127,6 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                 ++c.nodes;                                     // recursive call; its unit_propagate is a no-op
             } else if (!leaf) {                                // REF.py:208-213, as formula + [[var]]
                 const uint32_t v = r.best_var;
-                if (SPL && ((++dchk & SPLIT_MASK) == 0u)) {
-                    if (is_task && uniform_u32(ld_agent(&slot_ref(A, task).f->cancel))) {
-                        status = SATMI_DPLL_TIMEOUT;           // abandoned: the donor found its model first
-                        state = ST_DONE;
-                        continue;
-                    }
-                    if (dchk >= SPL->warm && uniform_i32(ld_agent(&SPL->want)) > 0)
-                        try_donate<K>(A, S, depth, b, dst, nd);
-                }
                 ep = next_decision_epoch<K>(S, n, ep);
                 if (ln == 0) {
                     S.fvar[depth] = (C)v;
@@ -1231,16 +1226,31 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
             }
         }
         if (__builtin_expect(c.nodes >= next_event, 0) && state != ST_DONE) {
-            const uint64_t total = flush_counters(ctr, c, flushed);
-            if (A.node_limit > 0 && total > (uint64_t)A.node_limit) {
-                status = SATMI_DPLL_NODE_LIMIT;
-                state = ST_DONE;
-            } else if (A.time_limit_ticks && __builtin_amdgcn_s_memrealtime() - t0 > A.time_limit_ticks) {
-                status = SATMI_DPLL_TIMEOUT;
-                state = ST_DONE;
-            } else {
-                next_event = next_event_after(A, total);
+            if (SPL) {
+                // between nodes every decision frame below depth is complete,
+                // so the shallowest open one can be donated here
+                ++nchk;
+                if (is_task && uniform_u32(ld_agent(&slot_ref(A, task).f->cancel))) {
+                    status = SATMI_DPLL_TIMEOUT;               // abandoned: the donor found its model first
+                    state = ST_DONE;
+                    continue;
+                }
+                if (nchk * SPLIT_CHECK_NODES >= SPL->warm && uniform_i32(ld_agent(&SPL->want)) > 0)
+                    try_donate<K>(A, S, depth, b, dst, nd);
             }
+            if (!SPL || c.nodes >= next_flush) {
+                const uint64_t total = flush_counters(ctr, c, flushed);
+                if (A.node_limit > 0 && total > (uint64_t)A.node_limit) {
+                    status = SATMI_DPLL_NODE_LIMIT;
+                    state = ST_DONE;
+                } else if (A.time_limit_ticks && __builtin_amdgcn_s_memrealtime() - t0 > A.time_limit_ticks) {
+                    status = SATMI_DPLL_TIMEOUT;
+                    state = ST_DONE;
+                } else {
+                    next_flush = next_event_after(A, total);
+                }
+            }
+            next_event = SPL ? min(next_flush, c.nodes + SPLIT_CHECK_NODES) : next_flush;
         }
     }
 #ifdef SATMI_PHASE_STAMPS

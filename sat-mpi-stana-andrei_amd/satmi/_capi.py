@@ -49,9 +49,9 @@ def set_split(enable, helpers_per_cu=0):
     check(load().satmi_dpll_set_split(int(enable), int(helpers_per_cu)), "satmi_dpll_set_split")
 
 
-def set_split_warmup(decisions=-1):
-    """Decisions a search makes before it may donate a branch (-1 = the library default)."""
-    check(load().satmi_dpll_set_split_warmup(int(decisions)), "satmi_dpll_set_split_warmup")
+def set_split_warmup(nodes=-1):
+    """Nodes a search visits before it may donate a branch (-1 = the library default)."""
+    check(load().satmi_dpll_set_split_warmup(int(nodes)), "satmi_dpll_set_split_warmup")
 
 
 def split_stats(stream=None):
