@@ -102,6 +102,24 @@ def parse():
     return a
 
 
+def init_ranks():
+    """One process per GPU (torchrun env): (world, rank, local device).  The
+    collective backend is RCCL ("nccl"); SATMI_DIST_BACKEND=gloo rehearses the
+    multi-rank path with several ranks on fewer GPUs (device = LOCAL_RANK mod
+    the visible GPUs) -- identical to the default on one rank per GPU."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    if world > 1:
+        torch.cuda.set_device(local)
+        backend = os.environ.get("SATMI_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local
+
+
 def host_cores():
     """CPU cores this job may use: the box's share (OMP_NUM_THREADS is set to it
     on the GPU box; os.cpu_count() there shows the whole machine), else the
@@ -252,12 +270,7 @@ def saturation_main(args):
     from satmi.dp import last_stats as dp_stats
     from satmi.resolution import last_stats as res_stats
     from satmi.resolution import resolve
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local = init_ranks()
     torch.cuda.set_device(local)
     holes, npass = SATURATION[args.workload]
     f = cnf.pigeonhole(holes)
@@ -331,12 +344,7 @@ def main():
         # one hardware queue per stream (+ the null stream's) so the launches run
         # concurrently; HIP reads this when the runtime starts, below
         os.environ["GPU_MAX_HW_QUEUES"] = str(NS + 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local = init_ranks()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     L = _capi.load()
