@@ -594,7 +594,10 @@ __device__ Choice choose(const SLds<K, C> &S, int n) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     int npure = 0;
-    uint32_t maxc = 0;
+    // per lane: its largest count and, among its variables with that count,
+    // the smallest first position (one pass; the wave's winner is the smallest
+    // first position among the lanes holding the wave's largest count)
+    uint32_t lmax = 0, lbest = NONE32;
     // predicated (no exec-mask branches): lanes past n read variable n's words
     for (int v0 = 1; v0 <= n; v0 += 64) {
         const int v = v0 + ln;
@@ -602,26 +605,19 @@ __device__ Choice choose(const SLds<K, C> &S, int n) {
         const bool live = (v <= n) & var_free(S.lv, vc);
         const uint32_t c = S.cnt[vc];
         const uint32_t p = c & 0xFFFFu, q = c >> 16;
-        maxc = live ? max(maxc, p + q) : maxc;
-        const bool pure = live & ((p + q) != 0u) & ((p == 0u) | (q == 0u));
         const uint32_t f = S.first[vc];
+        const bool better = live & ((p + q > lmax) | ((p + q == lmax) & (f < lbest)));
+        lmax = better ? p + q : lmax;
+        lbest = better ? f : lbest;
+        const bool pure = live & ((p + q) != 0u) & ((p == 0u) | (q == 0u));
         const uint64_t mk = __ballot(pure);
         if (pure) S.plist[npure + __popcll(mk & lt)] = f;
         npure += __popcll(mk);
     }
-    maxc = wave_max_u32(maxc);
+    const uint32_t maxc = wave_max_u32(lmax);
     uint32_t best = 0;
     if (npure == 0 && maxc > 0) {
-        uint32_t bestf = NONE32;
-        for (int v0 = 1; v0 <= n; v0 += 64) {
-            const int v = v0 + ln;
-            const uint32_t vc = (uint32_t)min(v, n);
-            const uint32_t c = S.cnt[vc];
-            const bool best_here = (v <= n) & var_free(S.lv, vc) & ((c & 0xFFFFu) + (c >> 16) == maxc);
-            const uint32_t fv = S.first[vc];
-            bestf = best_here ? min(bestf, fv) : bestf;
-        }
-        bestf = wave_min_u32(bestf);
+        const uint32_t bestf = wave_min_u32(lmax == maxc ? lbest : NONE32);
         best = uniform_u32(field<K>(S.cls[bestf >> 3], (int)(bestf & 7u)) >> 1);
     }
     for (int v = ln; v <= n; v += 64) {
