@@ -606,6 +606,8 @@ __device__ Choice choose(const SLds<K, C> &S, int n) {
         const uint32_t c = S.cnt[vc];
         const uint32_t p = c & 0xFFFFu, q = c >> 16;
         const uint32_t f = S.first[vc];
+        S.cnt[vc] = 0u;   // cleared for the next scan as soon as read
+        S.first[vc] = NONE32;
         const bool better = live & ((p + q > lmax) | ((p + q == lmax) & (f < lbest)));
         lmax = better ? p + q : lmax;
         lbest = better ? f : lbest;
@@ -620,10 +622,8 @@ __device__ Choice choose(const SLds<K, C> &S, int n) {
         const uint32_t bestf = wave_min_u32(lmax == maxc ? lbest : NONE32);
         best = uniform_u32(field<K>(S.cls[bestf >> 3], (int)(bestf & 7u)) >> 1);
     }
-    for (int v = ln; v <= n; v += 64) {
-        S.cnt[v] = 0u;
-        S.first[v] = NONE32;
-    }
+    S.cnt[0] = 0u;   // variable 0: the padding slots' counts (never read)
+    S.first[0] = NONE32;
     wave_sync();
     return {npure, best};
 }
