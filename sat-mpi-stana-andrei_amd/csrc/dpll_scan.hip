@@ -1103,7 +1103,10 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
             } else {
                 state = ST_ANALYZE;
             }
-        } else if (state == ST_ANALYZE) {
+        }
+        // no event test between propagation and analysis: the node count
+        // only moves in the analysis, so the test after it sees the same
+        if (state == ST_ANALYZE) {
             bool leaf = false;
             Choice r{0, 0u};
             ph.mark(PH_OTHER);
