@@ -507,7 +507,8 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
         ++rounds;
         const int rs = tl;
         const uint32_t bep = ep;   // the batch's epoch
-        for (int k0 = 0; k0 < nu; k0 += 64) {
+        int k0 = 0;
+        do {   // nu > 0: at least one step
             const int k = k0 + ln;
             const bool valid = k < nu;
             const uint32_t code = (uint32_t)S.snap[valid ? k : 0];   // predicated loads
@@ -521,7 +522,8 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             S.trail[tl + __popcll(mk & (first ? lt : ~0ull))] = (C)code;
             lv_assign(S.lv, first ? code : CODE_DUMMY);
             tl += __popcll(mk);
-        }
+            k0 += 64;
+        } while (k0 < nu);
         wave_sync();
         ph.mark(PH_ASSIGN);
         const int nassign = tl - rs;
@@ -599,7 +601,7 @@ __device__ Choice choose(const SLds<K, C> &S, int n) {
     // first position among the lanes holding the wave's largest count)
     uint32_t lmax = 0, lbest = NONE32;
     // predicated (no exec-mask branches): lanes past n read variable n's words
-    for (int v0 = 1; v0 <= n; v0 += 64) {
+    auto step = [&](int v0) {
         const int v = v0 + ln;
         const uint32_t vc = (uint32_t)min(v, n);
         const bool live = (v <= n) & var_free(S.lv, vc);
@@ -615,6 +617,12 @@ __device__ Choice choose(const SLds<K, C> &S, int n) {
         const uint64_t mk = __ballot(pure);
         if (pure) S.plist[npure + __popcll(mk & lt)] = f;
         npure += __popcll(mk);
+    };
+    if constexpr (sizeof(C) == 1) {   // byte trail codes: n <= 127, two steps at most, no loop
+        if (n >= 1) step(1);
+        if (n >= 65) step(65);
+    } else {
+        for (int v0 = 1; v0 <= n; v0 += 64) step(v0);
     }
     const uint32_t maxc = wave_max_u32(lmax);
     uint32_t best = 0;
