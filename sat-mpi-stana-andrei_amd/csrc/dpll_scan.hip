@@ -996,7 +996,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     const int mpad = padded_clauses(m);
     const int L = A.clause_lit_begin[ce] - A.clause_lit_begin[cb];
     const int n = A.inst_nvars[b];
-    const bool is_task = task >= 0;
+    const bool is_task = SPLIT && task >= 0;   // the unsplit form has no donated tasks
     int64_t *ctr = is_task ? slot_ref(A, task).h->ctr : A.counters + (int64_t)b * SATMI_NCOUNTERS;
     bool bad = m > A.lay.mcap || n > A.lay.ncap || n < 0 || L > 65535 || (INC && L > A.occ_cap);
     if (!bad) {
@@ -1176,7 +1176,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                 for (int i = ft + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
                 tl = ft;
                 wave_sync();
-                if (!(fv & SLds<K, C>::PHASE_BIT) && (ftw & DON)) {
+                if (SPLIT && !(fv & SLds<K, C>::PHASE_BIT) && (ftw & DON)) {
                     // the False branch was donated: take its result
                     --nd;
                     const int s = uniform_i32(dst[nd]);
@@ -1265,7 +1265,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     if (!is_task && A.root_lits && A.sol_stride >= 16 && ln < 8)
         ((int64_t *)(A.root_lits + (int64_t)b * A.sol_stride))[ln] = (int64_t)ph.acc[ln];
 #endif
-    if (nd > 0) cancel_donations(A, dst, nd);   // a model (or a cancellation) came first
+    if (SPLIT && nd > 0) cancel_donations(A, dst, nd);   // a model (or a cancellation) came first
     flush_counters(ctr, c, flushed);
     const int64_t ticks = (int64_t)(__builtin_amdgcn_s_memrealtime() - t_start);
     if (is_task) {
