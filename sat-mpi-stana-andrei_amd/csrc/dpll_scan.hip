@@ -503,9 +503,11 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
                           uint32_t &rounds, PhaseClock &ph) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
+    int e = INT_MAX;   // set: the round that emptied a clause (handled after the loop)
+    int rs = tl;
     while (nu > 0) {
         ++rounds;
-        const int rs = tl;
+        rs = tl;
         const uint32_t bep = ep;   // the batch's epoch
         int k0 = 0;
         do {   // nu > 0: at least one step
@@ -527,33 +529,31 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
         wave_sync();
         ph.mark(PH_ASSIGN);
         const int nassign = tl - rs;
-        int e = INT_MAX;
         const int nu_next = INC ? inc_units<K>(S, (mpad + 31) >> 5, rs, tl, ++ep, bep, &e)
                                 : scan_units<K>(S, mpad, ++ep, bep, &e);
         ph.mark(PH_UNITS);
-        if (e != INT_MAX) {
-            // the reference stopped at snapshot index e: keep the prefix of the
-            // batch stamped <= e (the batch is in stamp order)
-            int keep = 0;
-            for (int i0 = rs; i0 < tl; i0 += 64) {
-                const int i = i0 + ln;
-                const bool p = i < tl && (int)stamp_index(S.ts[S.trail[i] >> 1]) <= e;
-                keep += __popcll(__ballot(p));
-            }
-            const int cut = rs + keep;
-            for (int i = cut + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
-            wave_sync();
-            tl = cut;
-            props += keep - (dec ? 1 : 0);
-            ph.mark(PH_CONFLICT);
-            return true;
-        }
+        if (e != INT_MAX) break;
         props += nassign - (dec && nassign > 0 ? 1 : 0);
         dec = false;
         if (nassign == 0) break;   // `changed` stayed False (REF.py:141-142)
         nu = nu_next;
     }
-    return false;
+    if (e == INT_MAX) return false;
+    // the reference stopped at snapshot index e of the last batch, trail[rs,
+    // tl): keep the prefix stamped <= e (the batch is in stamp order)
+    int keep = 0;
+    for (int i0 = rs; i0 < tl; i0 += 64) {
+        const int i = i0 + ln;
+        const bool p = i < tl && (int)stamp_index(S.ts[S.trail[i] >> 1]) <= e;
+        keep += __popcll(__ballot(p));
+    }
+    const int cut = rs + keep;
+    for (int i = cut + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
+    wave_sync();
+    tl = cut;
+    props += keep - (dec ? 1 : 0);
+    ph.mark(PH_CONFLICT);
+    return true;
 }
 
 // literal_sign / var_counts scan (REF.py:174-179, :198-203): every free
