@@ -1166,7 +1166,33 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                 }
             }
         }
-        if (state == ST_BACKTRACK) {
+        if (!SPLIT && state == ST_BACKTRACK) {
+            // unwind the finished frames (both branches run) with one scalar
+            // read each, then clear the trail above the open frame once
+            state = ST_DONE;
+            int top = depth - 1;
+            while (top >= 0 && (uniform_u32(S.fvar[top]) & SLds<K, C>::PHASE_BIT)) --top;
+            depth = top + 1;
+            if (top >= 0) {
+                const uint32_t fv = uniform_u32(S.fvar[top]);
+                const int ft = (int)uniform_u32(S.ftrail[top]);
+                for (int i = ft + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
+                tl = ft;
+                ep = next_decision_epoch<K>(S, n, ep);
+                if (ln == 0) {
+                    S.fvar[top] = (C)(fv | SLds<K, C>::PHASE_BIT);
+                    S.snap[0] = (C)((fv << 1) | 1u);           // False
+                    S.ts[fv] = stamp(ep, 0u);
+                }
+                ++c.decisions;
+                ++c.nodes;
+                nu = 1;
+                dec_round = true;
+                state = ST_PROPAGATE;
+                wave_sync();
+            }
+        }
+        if (SPLIT && state == ST_BACKTRACK) {
             state = ST_DONE;
             while (depth > 0) {
                 const int top = depth - 1;
