@@ -1194,15 +1194,18 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
         }
         if (SPLIT && state == ST_BACKTRACK) {
             state = ST_DONE;
-            while (depth > 0) {
+            for (;;) {
+                // unwind the finished frames with one scalar read each
+                while (depth > 0 && (uniform_u32(S.fvar[depth - 1]) & SLds<K, C>::PHASE_BIT)) --depth;
+                if (depth == 0) break;
                 const int top = depth - 1;
-                const uint32_t fv = uniform_u32(S.fvar[top]);
+                const uint32_t fv = uniform_u32(S.fvar[top]);   // its False branch has not run here
                 const uint32_t ftw = uniform_u32(S.ftrail[top]);
                 const int ft = (int)(ftw & ~DON);
                 for (int i = ft + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
                 tl = ft;
                 wave_sync();
-                if (SPLIT && !(fv & SLds<K, C>::PHASE_BIT) && (ftw & DON)) {
+                if (ftw & DON) {
                     // the False branch was donated: take its result
                     --nd;
                     const int s = uniform_i32(dst[nd]);
@@ -1240,22 +1243,19 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                         break;
                     }
                 }
-                if (!(fv & SLds<K, C>::PHASE_BIT)) {
-                    ep = next_decision_epoch<K>(S, n, ep);
-                    if (ln == 0) {
-                        S.fvar[top] = (C)(fv | SLds<K, C>::PHASE_BIT);
-                        S.snap[0] = (C)((fv << 1) | 1u);           // False
-                        S.ts[fv] = stamp(ep, 0u);
-                    }
-                    ++c.decisions;
-                    ++c.nodes;
-                    nu = 1;
-                    dec_round = true;
-                    state = ST_PROPAGATE;
-                    wave_sync();
-                    break;
+                ep = next_decision_epoch<K>(S, n, ep);
+                if (ln == 0) {
+                    S.fvar[top] = (C)(fv | SLds<K, C>::PHASE_BIT);
+                    S.snap[0] = (C)((fv << 1) | 1u);               // False
+                    S.ts[fv] = stamp(ep, 0u);
                 }
-                --depth;
+                ++c.decisions;
+                ++c.nodes;
+                nu = 1;
+                dec_round = true;
+                state = ST_PROPAGATE;
+                wave_sync();
+                break;
             }
         }
         if (__builtin_expect(c.nodes >= next_event, 0) && state != ST_DONE) {
