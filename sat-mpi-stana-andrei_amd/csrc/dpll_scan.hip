@@ -312,7 +312,7 @@ template <int K, typename C>
 __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t ep, uint32_t bep, int *empty_at) {
     using W = typename Pack<K>::W;
     const int ln = lane_id();
-    if (tl - rs <= 64) {
+    if (__builtin_expect(tl - rs <= 64, 1)) {
         // lane b: the b-th batch literal's negation and its occurrence list
         // predicated (no exec-mask branch): lanes past the batch read entry rs
         const bool inb = ln < tl - rs;
@@ -323,7 +323,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
         const int excl = incl - len;
         const int delta = ob - excl;
         const int total = lane63(incl);
-        if (total <= 64) {
+        if (__builtin_expect(total <= 64, 1)) {
             // one touched clause per lane
             int d = __builtin_amdgcn_readlane(delta, 0);
             if (tl - rs > 1)   // one batch literal: lane 0's list is the whole range
@@ -352,7 +352,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const bool unit = open && nf == 1u;
             const uint64_t um = __ballot(unit);
             const int nun = __popcll(um);
-            if (nun <= FAST_UNITS) {
+            if (__builtin_expect(nun <= FAST_UNITS, 1)) {
                 // a clause reached from two batch literals is one snapshot entry
                 bool dup = false;
                 uint64_t dm = um;
@@ -532,7 +532,7 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
         const int nu_next = INC ? inc_units<K>(S, (mpad + 31) >> 5, rs, tl, ++ep, bep, &e)
                                 : scan_units<K>(S, mpad, ++ep, bep, &e);
         ph.mark(PH_UNITS);
-        if (e != INT_MAX) break;
+        if (__builtin_expect(e != INT_MAX, 0)) break;
         props += nassign - (dec && nassign > 0 ? 1 : 0);
         dec = false;
         if (nassign == 0) break;   // `changed` stayed False (REF.py:141-142)
