@@ -462,6 +462,22 @@ struct DpStats {
 DpStats g_dp_stats;
 
 // ordered compaction of flag[n] into out (indices); returns the count
+// compact() without the count read-back: `out` is sized for all n, the count
+// lands in *count_dev; several of these share one read-back (same stream, so
+// pos / tiles are reused in order)
+int compact_deferred(const int64_t *flag, int64_t n, Buf &pos, Buf &tiles, int64_t *count_dev, Buf &out,
+                     hipStream_t s) {
+    DP_TRY(pos.need(8 * (size_t)std::max<int64_t>(n, 1)));
+    DP_TRY(tiles.need(8 * (size_t)((n + SCAN_TILE - 1) / SCAN_TILE + 1)));
+    DP_TRY(out.need(8 * (size_t)std::max<int64_t>(n, 1)));
+    DP_TRY(exclusive_scan(flag, pos.as<int64_t>(), n, tiles.as<int64_t>(), count_dev, s));
+    if (n > 0)
+        hipLaunchKernelGGL(dp_compact_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, flag, pos.as<int64_t>(), n,
+                           out.as<int64_t>());
+    SATMI_HIP(hipGetLastError());
+    return SATMI_OK;
+}
+
 int compact(const int64_t *flag, int64_t n, Buf &pos, Buf &tiles, Buf &grand, Buf &out, int64_t *count,
             hipStream_t s) {
     *count = 0;
@@ -521,7 +537,7 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     hipStream_t s = nullptr;
 
     Buf d_off, d_lits, d_v2d, d_d2v, flags, misc, firstpos, order, popscratch, base, usedtmp;
-    Buf fpos, fneg, frem, plist, nlist, rlist, scanpos, tiles, grand, rbits, nontaut, ntlist, kept, klist, kpos,
+    Buf fpos, fneg, frem, plist, nlist, rlist, scanpos, tiles, grand, counts3, rbits, nontaut, ntlist, kept, klist, kpos,
         sizes, offs;
     Gen g[2];
     Img A, B, R;
@@ -619,10 +635,16 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         DP_TRY(frem.need(8 * (size_t)ncl));
         hipLaunchKernelGGL(dp_split_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, Lc, ncl, W, d,
                            fpos.as<int64_t>(), fneg.as<int64_t>(), frem.as<int64_t>());
-        int64_t np = 0, nn = 0, nr = 0;
-        DP_TRY(compact(fpos.as<int64_t>(), ncl, scanpos, tiles, grand, plist, &np, s));
-        DP_TRY(compact(fneg.as<int64_t>(), ncl, scanpos, tiles, grand, nlist, &nn, s));
-        DP_TRY(compact(frem.as<int64_t>(), ncl, scanpos, tiles, grand, rlist, &nr, s));
+        // the three lists with one count read-back
+        DP_TRY(counts3.need(3 * sizeof(int64_t)));
+        int64_t *c3 = counts3.as<int64_t>();
+        DP_TRY(compact_deferred(fpos.as<int64_t>(), ncl, scanpos, tiles, c3 + 0, plist, s));
+        DP_TRY(compact_deferred(fneg.as<int64_t>(), ncl, scanpos, tiles, c3 + 1, nlist, s));
+        DP_TRY(compact_deferred(frem.as<int64_t>(), ncl, scanpos, tiles, c3 + 2, rlist, s));
+        int64_t h3[3] = {0, 0, 0};
+        SATMI_HIP(hipMemcpyAsync(h3, c3, sizeof(h3), hipMemcpyDeviceToHost, s));
+        SATMI_HIP(hipStreamSynchronize(s));
+        const int64_t np = h3[0], nn = h3[1], nr = h3[2];
         const int64_t npairs = np * nn;
         // resolvent bitsets + flags (REF.py:111-119)
         int64_t m = 0;
@@ -768,6 +790,10 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             }
             h_rec_step_off[steps] = rec_clauses;
         }
+        // the set-model overflow flag (misc[0]) of this step is read with the
+        // next step's pop, or after the loop
+    }
+    {
         int32_t ovf2 = 0;
         SATMI_HIP(hipMemcpyAsync(&ovf2, misc.p, 4, hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
@@ -776,7 +802,6 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             return SATMI_ERR_TOO_LARGE;
         }
     }
-    SATMI_HIP(hipStreamSynchronize(s));
     {
         unsigned long long tests = 0;
         SATMI_HIP(hipMemcpy(&tests, misc.as<char>() + 40, 8, hipMemcpyDeviceToHost));
