@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: batched DPLL on random 3-SAT n=100, alpha=4.26 (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--per-gpu B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload P]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 A step = one pass of the hot path (csrc/dpll_scan.hip, SOUND mode, stop at the
@@ -10,12 +10,17 @@ first model: the SAT/UNSAT decision) over one batch of synthetic uniform random
 step's verdict/counter totals.  Consecutive steps alternate between two HIP
 streams (and two resident batches), so one batch's tail overlaps the next
 batch's start; the timed region still brackets all K steps with barrier +
-synchronize.  The batch is BASELINE.json configs[2]: 262,144
-instances of n=100, alpha=4.26 per step, sharded across the ranks with no
-data-path collective (strong scaling: 262,144 / N instances per GPU).
+synchronize.  The batch is BASELINE.json configs[2]: 262,144 instances of
+n=100, alpha=4.26 per step, sharded across the ranks with no data-path
+collective (strong scaling: 262,144 / N instances per GPU).  The batch is
+generated in chunks of CHUNK instances, chunk c from seed + c, and a rank
+materialises only the chunks of its shard: every N solves the same instances,
+and the line's `verdict_sha` (the per-instance verdicts of the last step,
+gathered over RCCL) is the same for every N.
 
---workload selects the other BASELINE.json configs (parity-test cases, measured
-with the same harness; the default line is configs[2]):
+--workload selects the other BASELINE.json configs (the default line is
+configs[2]; at N = 1 the default run also measures every other config in a
+child process after the headline -- the line's `configs` object):
     3sat-n50   configs[1]: 4,096 instances of n=50, alpha=4.26
     uf250      configs[4]: uf250-1065 shape (random 3-SAT n=250, m=1065),
                node-capped search (--node-limit, default 20,000 calls/instance)
@@ -25,16 +30,23 @@ with the same harness; the default line is configs[2]):
                (30 variables, 81 clauses; every step's resolvents, tautology
                and subsumption filter on the GPU) -- solves/s
     php-res    configs[3]: resolution saturation of PHP(4,3) (pair kernel +
-               sort dedup), its first 4 passes (171,392 derived clauses; the
+               hash dedup), its first 4 passes (171,392 derived clauses; the
                5th pass would resolve 1.5e10 pairs) -- derived clauses/s
+    cdcl       the reference's CDCLSolver (REF.py:217-384) on 4,096 menu-sized
+               formulas (generate_large_formula(80, 3, 15), REF.py:21-29, the
+               shape of rezultat.txt:178-188), <= 10,000 iterations each --
+               formulas/s
 For the node-capped workloads the headline value is unit-props/s.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -44,14 +56,13 @@ import torch  # noqa: E402  (before libsatmi: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
 from satmi import _capi, cnf  # noqa: E402
-from satmi.shard import shard_range  # noqa: E402
+from satmi.shard import gather_verdicts, shard_range  # noqa: E402
 
 METRIC = "instances solved/sec, random 3-SAT n=100 α=4.26; unit-props/sec; HBM GB/s"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SHADER_CLOCK_HZ = 2.4e9        # MI355X_MICROARCH.md: peak engine clock (the LDS-issue peak of dp_roofline)
-KERNELS = {_capi.KERNEL_SCAN: "dpll_scan_kernel", _capi.KERNEL_INC: "dpll_scan_kernel (incremental rounds)",
-           _capi.KERNEL_GENERAL: "dpll_batch_kernel"}
-
+CHUNK = 4096                   # instances per generation chunk (chunk c drawn from seed + c)
+FIX_NCAP, FIX_MCAP = 127, 448  # dpll_fixed_kernel's shape class (csrc/dpll_scan.hip)
 
 # workload presets: (total instances per step, n, alpha, k, node_limit, BASELINE config)
 WORKLOADS = {
@@ -60,16 +71,30 @@ WORKLOADS = {
     "uf250": (6144, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,072 resident waves
     "5sat-n200": (1536, 200, 21.117, 5, 20000, "configs[4]"),  # 2 x the 768 resident waves
 }
-# configs[3] presets: (holes, clause_limit) -- one formula per step, host-array C ABI
-SATURATION = {"php-dp": (5, 0), "php-res": (3, 4)}   # (holes, resolution passes)
+# configs[3] presets: (holes, resolution passes) -- one formula per step, host-array C ABI
+SATURATION = {"php-dp": (5, 0), "php-res": (3, 4)}
+# CDCL preset: (formulas per step, clauses, max literals per clause, variables, max_iter, seed)
+CDCL = {"cdcl": (4096, 80, 3, 15, 10000, 1234)}
+
+# the secondary legs of the default N = 1 line: (name, workload, extra args)
+LEGS = [
+    ("configs[1] 2 streams", "3sat-n50", ["--streams", "2", "--steps", "32", "--warmup", "4"]),
+    ("configs[1] 16 streams", "3sat-n50", ["--streams", "16", "--steps", "128", "--warmup", "16"]),
+    ("configs[3] php-dp", "php-dp", ["--steps", "40", "--warmup", "3"]),
+    ("configs[3] php-res", "php-res", ["--steps", "20", "--warmup", "2"]),
+    ("configs[4] uf250", "uf250", ["--steps", "4", "--warmup", "1"]),
+    ("configs[4] 5sat-n200", "5sat-n200", ["--steps", "4", "--warmup", "1"]),
+    ("cdcl", "cdcl", ["--steps", "3", "--warmup", "1"]),
+]
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(SATURATION), default="3sat-n100")
+    p.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(SATURATION) + sorted(CDCL),
+                   default="3sat-n100")
     p.add_argument("--total", type=int, default=None, help="instances per step, all ranks")
     p.add_argument("--n", type=int, default=None)
     p.add_argument("--alpha", type=float, default=None)
@@ -78,6 +103,9 @@ def parse():
     p.add_argument("--seed", type=int, default=20251016)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-legs", action="store_true", help="only the headline workload (no `configs` object)")
+    p.add_argument("--legs-only", action="store_true", help=argparse.SUPPRESS)   # the child of the default run
+    p.add_argument("--leg-cpu-seconds", type=float, default=4.0, help="CPU baseline budget of each leg")
     p.add_argument("--profile-steps", action="store_true", help="no warmup/cpu leg (for rocprofv3 runs)")
     p.add_argument("--kernel", choices=("auto", "inc", "scan", "general"), default="auto",
                    help="DPLL kernel policy (satmi_dpll_set_kernel); auto = incremental clause kernel")
@@ -90,15 +118,14 @@ def parse():
     p.add_argument("--streams", type=int, default=None, choices=range(1, 17),
                    help="HIP streams (each with its own resident batch) the steps rotate over (default: 16 for "
                         "3sat-n50, whose 4,096 short searches leave most CU slots idle for a launch's 2 ms, else 2)")
-    a = p.parse_args()
-    if a.workload in SATURATION:
-        return a
-    total, n, alpha, k, node_limit, a.config_name = WORKLOADS[a.workload]
-    a.total = total if a.total is None else a.total
-    a.n = n if a.n is None else a.n
-    a.alpha = alpha if a.alpha is None else a.alpha
-    a.k = k if a.k is None else a.k
-    a.node_limit = node_limit if a.node_limit is None else a.node_limit
+    a = p.parse_args(argv)
+    if a.workload in WORKLOADS:
+        total, n, alpha, k, node_limit, a.config_name = WORKLOADS[a.workload]
+        a.total = total if a.total is None else a.total
+        a.n = n if a.n is None else a.n
+        a.alpha = alpha if a.alpha is None else a.alpha
+        a.k = k if a.k is None else a.k
+        a.node_limit = node_limit if a.node_limit is None else a.node_limit
     return a
 
 
@@ -110,7 +137,7 @@ def init_ranks():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-    if world > 1:
+    if world > 1 and not dist.is_initialized():
         torch.cuda.set_device(local)
         backend = os.environ.get("SATMI_DIST_BACKEND", "nccl")
         if backend == "nccl":
@@ -128,14 +155,26 @@ def host_cores():
     return max(1, int(env) if env else len(os.sched_getaffinity(0)))
 
 
+def cpu_pool(kind, icb, clb, lits, seconds, param):
+    """oracle/cpu_pool.py as a child process (never touches the GPU), one worker
+    per host core, on the CSR sample given."""
+    import numpy as np
+    cores = host_cores()
+    with tempfile.TemporaryDirectory(prefix="satmi_cpu_") as tmp:
+        for name, arr in (("icb", icb), ("clb", clb), ("lits", lits)):
+            np.save(os.path.join(tmp, name + ".npy"), np.ascontiguousarray(arr, dtype=np.int32))
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("HIP_", "ROCR_", "HSA_", "GPU_"))}
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_pool.py"), kind, tmp, str(seconds),
+                              str(param), str(cores)], check=True, capture_output=True, text=True, env=env)
+    return json.loads(out.stdout.strip().splitlines()[-1]), cores
+
+
 def cpu_baseline(batch_host, seconds, node_limit):
     """The CPU oracle (oracle/, a C restatement of REF.py's DPLL, SOUND mode) on
     rank 0's host, on the same bench batch: one core (instances from the start
-    of the batch until `seconds` / 3 pass), then every core (oracle/cpu_pool.py
-    as a child process that never touches the GPU, one worker per core, for
-    `seconds`).  `value` is the all-cores rate; the one-core rate is beside it."""
-    import subprocess
-    import tempfile
+    of the batch until `seconds` / 3 pass), then every core (oracle/cpu_pool.py,
+    one worker per core, for `seconds`).  `value` is the all-cores rate; the
+    one-core rate is beside it."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -158,13 +197,7 @@ def cpu_baseline(batch_host, seconds, node_limit):
     icb = batch_host.inst_clause_begin[:nsamp + 1].astype(np.int32)
     clb = batch_host.clause_lit_begin[:int(icb[-1]) + 1].astype(np.int32)
     lits = batch_host.lits[:int(clb[-1])].astype(np.int32)
-    with tempfile.TemporaryDirectory(prefix="satmi_cpu_") as tmp:
-        for name, arr in (("icb", icb), ("clb", clb), ("lits", lits)):
-            np.save(os.path.join(tmp, name + ".npy"), arr)
-        env = {k: v for k, v in os.environ.items() if not k.startswith(("HIP_", "ROCR_", "HSA_"))}
-        out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_pool.py"), tmp, str(seconds),
-                              str(node_limit), str(cores)], check=True, capture_output=True, text=True, env=env)
-    pool = json.loads(out.stdout.strip().splitlines()[-1])
+    pool, cores = cpu_pool("dpll", icb, clb, lits, seconds, node_limit)
     rate = pool["unit_props_per_s"] if capped else pool["instances_per_s"]
     return {"value": rate, "unit": "unit-props/s" if capped else "instances/s",
             "cores": cores, "kind": "port",
@@ -175,14 +208,17 @@ def cpu_baseline(batch_host, seconds, node_limit):
             "single_core": one}
 
 
-def load_pmc(workload_key):
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_profile(name, key):
     try:
-        with open(path) as fh:
-            d = json.load(fh)
-        return d.get(workload_key)
+        with open(os.path.join(ROOT, "profiles", name)) as fh:
+            return json.load(fh).get(key)
     except (OSError, ValueError):
         return None
+
+
+def kernel_src_sha():
+    with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", "dpll_scan.hip"), "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
 def issue_roofline(preset, per_gpu, kernel_ms):
@@ -192,14 +228,7 @@ def issue_roofline(preset, per_gpu, kernel_ms):
     this run's live kernel time at the profiled effective clock.  Peaks: VALU 0.5
     wave-instructions / cycle / SIMD, SALU 1 / cycle / CU, LDS array 1 cycle /
     cycle / CU.  `stale` if the kernel source changed since the profile."""
-    import hashlib
-    try:
-        with open(os.path.join(ROOT, "profiles", "sq_issue.json")) as fh:
-            e = json.load(fh).get(f"{preset}_B{per_gpu}")
-        with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", "dpll_scan.hip"), "rb") as fh:
-            sha = hashlib.sha256(fh.read()).hexdigest()[:16]
-    except (OSError, ValueError):
-        return None
+    e = load_profile("sq_issue.json", f"{preset}_B{per_gpu}")
     if not e:
         return None
     cyc = e["effective_clock_hz"] * kernel_ms * 1e-3
@@ -212,139 +241,67 @@ def issue_roofline(preset, per_gpu, kernel_ms):
     return {"bound": bound, "achieved": a / (kernel_ms * 1e-3), "peak": p / (kernel_ms * 1e-3),
             "unit": unit + "/s", "frac": fr[bound], "fracs": fr,
             "lds_bank_conflict_share": e["lds_bank_conflict_cycles"] / e["lds_array_cycles"],
-            "clock_hz": e["effective_clock_hz"], "source": e["source"], "stale": e["kernel_src_sha256_16"] != sha}
+            "clock_hz": e["effective_clock_hz"], "source": e["source"],
+            "stale": e["kernel_src_sha256_16"] != kernel_src_sha()}
 
 
-def dp_roofline(stats, cus, clock_hz):
-    """Davis-Putnam (php-dp): the subsumption filter dominates (dp_subsume_tiled_kernel,
-    one lane per new clause, candidate keys broadcast from LDS).  Its binding
-    resource is the LDS issue pipe: one ds_read of a K-word key serves the 256
-    lanes of a workgroup, so a CU retires at most 64 / K subset tests per
-    cycle (64 lanes x one key word per LDS instruction per cycle).  achieved =
-    subset tests performed / the filter's device time (HIP events)."""
-    if not stats:
-        return None
-    tests = sum(s["subset_tests"] for s in stats) / len(stats)
-    ms = sum(s["subsume_ms"] for s in stats) / len(stats)
-    K = stats[-1]["words"]
-    if ms <= 0 or K <= 0:
-        return None
-    ach = tests / (ms * 1e-3)
-    peak = cus * clock_hz * 64.0 / K
-    return {"bound": "lds-issue", "achieved": ach, "peak": peak, "unit": "subset-tests/s", "frac": ach / peak,
-            "traffic": None, "kernel": "dp_subsume_tiled_kernel", "kernel_ms_per_step": ms,
-            "subset_tests_per_step": tests, "new_clauses_per_step": sum(s["new_clauses"] for s in stats) / len(stats),
-            "key_words": K, "clock_hz": clock_hz}
+def dpll_kernel_name(n, m, k, split):
+    """The kernel satmi_dpll_batch_device launches for this shape (csrc/dpll_scan.hip
+    scan_plan / dpll_scan_launch; `split` = the launch used the splitting form)."""
+    kern, _, _ = _capi.plan(n, m, m * k, k)
+    if kern == _capi.KERNEL_INC and k == 3 and n <= FIX_NCAP and m <= FIX_MCAP:
+        return f"dpll_fixed_kernel<{FIX_MCAP}, {'true' if split else 'false'}>"
+    return {_capi.KERNEL_SCAN: "dpll_scan_kernel (full scans)", _capi.KERNEL_INC: "dpll_scan_kernel (incremental rounds)",
+            _capi.KERNEL_GENERAL: "dpll_batch_kernel"}.get(kern, f"kernel {kern}")
 
 
-def saturation_roofline(workload, stats, last):
-    """Resolution (php-res): the dominant of its two kernels per step, timed by
-    HIP events on the library's stream (satmi_resolution_last_stats).  Claim
-    kernel (hash dedup): per candidate its key (8K B) read, one table slot
-    read + CAS (16 B), the occupant's key compared (8K B), flag + slot written
-    (16 B); pair kernel: per pair key i read (8K B), per candidate its key
-    written (8K B); K = 2 x 64-bit words per clause for <= 64 variables."""
-    if workload != "php-res" or not stats:
-        return None
-    K = 2   # PHP(4,3): 12 variables -> one word per sign
-    cand = sum(s["candidates"] for s in stats) / len(stats)
-    pairs = sum(s["pairs"] for s in stats) / len(stats)
-    cms = sum(s["claim_ms"] for s in stats) / len(stats)
-    pms = sum(s["pair_ms"] for s in stats) / len(stats)
-    claim_b = cand * (16 * K + 32)
-    pair_b = pairs * 8 * K + cand * 8 * K
-    name, b, ms = ("ht_cand_kernel (hash claims)", claim_b, cms) if cms >= pms else \
-        ("res_pairs_kernel", pair_b, pms)
-    ach = b / (ms * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "traffic": None, "kernel": name, "kernel_ms_per_step": ms, "algorithmic_bytes_per_step": b,
-            "candidates_per_step": cand, "pairs_per_step": pairs, "pair_ms_per_step": pms, "claim_ms_per_step": cms}
+def span_union_ms(spans, hz):
+    """Length of the union of [begin, end) launch intervals (device ticks) in ms."""
+    iv = sorted(spans)
+    tot, cur_b, cur_e = 0, None, None
+    for b, e in iv:
+        if cur_e is None or b > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_b
+            cur_b, cur_e = b, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        tot += cur_e - cur_b
+    return tot / hz * 1e3
 
 
-def saturation_main(args):
-    """configs[3]: Davis-Putnam / resolution saturation of a pigeonhole formula.
-    A step = one full satmi_dp_host / satmi_resolution_host call (host arrays in,
-    verdict out: the boundary these solvers have, REF.py:63-130).  Each rank
-    solves its own replica (one formula does not shard)."""
-    from satmi.dp import eliminate
-    from satmi.dp import last_stats as dp_stats
-    from satmi.resolution import last_stats as res_stats
-    from satmi.resolution import resolve
-    world, rank, local = init_ranks()
-    torch.cuda.set_device(local)
-    holes, npass = SATURATION[args.workload]
-    f = cnf.pigeonhole(holes)
-    if args.workload == "php-dp":
-        run = lambda: eliminate(f)                                  # noqa: E731
-        work = lambda r: 1                                          # noqa: E731
-        unit, metric_desc = "solves/s", f"Davis-Putnam elimination of PHP({holes + 1},{holes})"
-    else:
-        run = lambda: resolve(f, max_passes=npass)                  # noqa: E731
-        work = lambda r: sum(r["pass_new"])                         # noqa: E731
-        unit, metric_desc = "derived clauses/s", f"resolution saturation of PHP({holes + 1},{holes}), first {npass} passes"
-    for _ in range(0 if args.profile_steps else args.warmup):
-        run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    done = 0
-    last = None
-    stats = []
-    for _ in range(args.steps):
-        last = run()
-        done += work(last)
-        stats.append(res_stats() if args.workload == "php-res" else dp_stats())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    out = {"metric": METRIC, "value": done * world / elapsed, "unit": unit, "n_gpus": world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic: pigeonhole formula",
-           "config": {"workload": metric_desc + " (BASELINE configs[3]); replicas across ranks",
-                      "preset": args.workload, "parallelism": f"replicas x{world}"},
-           "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
-           "roofline": saturation_roofline(args.workload, stats, last) if args.workload == "php-res" else
-           dp_roofline(stats, torch.cuda.get_device_properties(local).multi_processor_count,
-                       SHADER_CLOCK_HZ)}
-    if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline and not args.profile_steps:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import oracle
-            t = time.perf_counter()
-            r = oracle.dp(f) if args.workload == "php-dp" else oracle.resolution(f, max_passes=npass)
-            dt = time.perf_counter() - t
-            w = 1 if args.workload == "php-dp" else sum(r["pass_new"])
-            if r["result"] != last["result"] or w != work(last):
-                raise SystemExit("bench: GPU and oracle disagree on the configs[3] workload")
-            cpu = {"value": w / dt, "unit": unit, "cores": 1, "kind": "port",
-                   "sample": f"one {metric_desc} by the oracle (oracle/*.c), single thread, {dt:.2f} s"}
-        out["cpu_baseline"] = cpu
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+def chunked_batch(b0, b1, n, m, k, seed, device):
+    """Instances [b0, b1) of the virtual batch whose chunk c (instances
+    [c*CHUNK, (c+1)*CHUNK)) is cnf.uniform_ksat_device(CHUNK, ..., seed + c):
+    only the chunks overlapping [b0, b1) are drawn, so a rank's shard equals
+    the same slice of the whole batch for every rank count."""
+    B = b1 - b0
+    if B <= 0:
+        raise ValueError("empty shard")
+    c0, c1 = b0 // CHUNK, (b1 - 1) // CHUNK + 1
+    parts = []
+    for c in range(c0, c1):
+        _, _, lits, _ = cnf.uniform_ksat_device(CHUNK, n, m, k, seed=seed + c, device=device)
+        lo = max(b0, c * CHUNK) - c * CHUNK
+        hi = min(b1, (c + 1) * CHUNK) - c * CHUNK
+        parts.append(lits.view(CHUNK, m * k)[lo:hi])
+    lits = torch.cat(parts).reshape(-1).contiguous()
+    icb = (torch.arange(B + 1, device=device, dtype=torch.int64) * m).to(torch.int32)
+    clb = (torch.arange(B * m + 1, device=device, dtype=torch.int64) * k).to(torch.int32)
+    nv = torch.full((B,), n, device=device, dtype=torch.int32)
+    return icb, clb, lits, nv
 
 
-def main():
-    args = parse()
-    if args.workload in SATURATION:
-        return saturation_main(args)
-    # measured (one MI355X, profiles/r02/final/streams.txt): 3sat-n50 3.83 M instances/s
-    # on 2 streams, 5.40 M on 3, 6.32 M on 4, 7.5 M on 8, 8.6 M on 12, 9.3 M on 16 (with
-    # --steps >= 8 x streams); configs[2] the same on 2, 3 or 4 streams, its N=8 share
-    # 496 k on 2 and 4, 463 k on 3
+def batch_seed(seed, j):
+    """Seed base of resident batch j (one per stream), the same for every rank count."""
+    return seed + 7919 * j
+
+
+def run_dpll(args, world, rank, local):
+    """One DPLL bench run (headline or leg): returns (line dict, host batch of the
+    last step for the CPU baseline or None)."""
     NS = args.streams or (16 if args.workload == "3sat-n50" else 2)
-    if NS > 3 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < NS + 1:
-        # one hardware queue per stream (+ the null stream's) so the launches run
-        # concurrently; HIP reads this when the runtime starts, below
-        os.environ["GPU_MAX_HW_QUEUES"] = str(NS + 1)
-    world, rank, local = init_ranks()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     L = _capi.load()
@@ -358,8 +315,9 @@ def main():
     b0, b1 = shard_range(args.total, world, rank)   # this rank's contiguous shard of the step's batch
     B = b1 - b0
     m = int(round(args.alpha * n))
-    # NS distinct resident batches per rank, rotated step to step
-    batches = [cnf.uniform_ksat_device(B, n, m, k, seed=args.seed + 1000 * rank + j, device=dev) for j in range(NS)]
+    # NS distinct resident batches, rotated step to step (batch j: the virtual
+    # batch of seed base batch_seed(seed, j), this rank's slice of it)
+    batches = [chunked_batch(b0, b1, n, m, k, batch_seed(args.seed, j), dev) for j in range(NS)]
     # NS streams, each with its own batch and output buffers: step j runs on
     # stream j % NS, so the next batch's waves take the CU slots that the
     # current batch's tail (its longest searches) leaves idle.  Launches on one
@@ -372,9 +330,7 @@ def main():
                      torch.zeros((B, _capi.NCOUNTERS), dtype=torch.int64, device=dev),
                      torch.zeros(B, dtype=torch.int32, device=dev),
                      torch.zeros((B, n), dtype=torch.int32, device=dev)))
-
     b_count = torch.tensor(B, device=dev, dtype=torch.int64)   # made once: a host->device copy per step would block
-
     spans = torch.zeros((max(args.steps, 1), 2), dtype=torch.int64, device=dev)
 
     def step(j, evs=None):
@@ -426,17 +382,22 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     # launch duration of the DPLL kernel: its own clocks (first wave start to
-    # last wave end, s_memrealtime), which stay exact while the two streams'
-    # launches overlap; the HIP-event bracket on each stream is reported beside
-    # it (it also counts the time a launch waits behind the other stream's tail)
+    # last wave end, s_memrealtime), exact while the streams' launches overlap;
+    # the HIP-event bracket on each stream is reported beside it (it also counts
+    # the time a launch waits behind the other stream's tail).  The union of
+    # the launch spans over the timed region is the time some launch ran: per
+    # step it is <= ms_per_step (the overlap is what the streams buy).
     sp = spans.cpu().numpy().astype("uint64")
     hz = _capi.wallclock_hz()
-    span_ms = [float((int(e) - (~int(b) & (2**64 - 1))) / hz * 1e3) for b, e in sp[:args.steps]]
+    iv = [(int(~int(b) & (2**64 - 1)), int(e)) for b, e in sp[:args.steps]]
+    span_ms = [(e - b) / hz * 1e3 for b, e in iv]
     kernel_ms = sum(span_ms) / len(span_ms)
+    union_ms = span_union_ms(iv, hz)
     kms = [a.elapsed_time(b) for a, b in evs]
     event_ms = sum(kms) / len(kms)
     totals = torch.stack(aggs).sum(dim=0)
-    status, counters, sol_len, sol_lits = outs[(args.steps - 1) % NS]
+    last = (args.steps - 1) % NS
+    status, counters, sol_len, sol_lits = outs[last]
     tot = totals.tolist()
     nsat, props, nodes, bad, written, ticks, all_inst = tot
     capped = args.node_limit > 0
@@ -462,24 +423,40 @@ def main():
     models_ok = all(models_ok_for(j) for j in range(max(0, args.steps - NS), args.steps))
     if not models_ok or bad:
         raise SystemExit(f"bench: invalid result (models_ok={models_ok}, limited={bad})")
-    icb, clb, lits, nv = batches[(args.steps - 1) % NS]
+    # the last step's per-instance verdicts gathered over the process group
+    # (RCCL all-gather): the same hash for every rank count
+    sat_last = (counters[:, 5] > 0).to(torch.int8)
+    verdicts, ctr_tot = gather_verdicts(sat_last, counters, args.total, device=dev)
+    seen = torch.ones(1, dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(seen)
+    verdict_sha = hashlib.sha256(verdicts.cpu().numpy().tobytes()).hexdigest()[:16]
+    icb, clb, lits, nv = batches[last]
 
     # roofline of the dominant kernel: algorithmic bytes per launch / average launch time
     read_bytes = B * (4 * m * k + 4 * m + 4 + 4) + 4
     write_bytes = B * (4 + 8 * _capi.NCOUNTERS) + written / all_inst * B
     alg_bytes = read_bytes + write_bytes
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    ach_excl = alg_bytes * args.steps / (union_ms * 1e-3) / 1e9
     workload = f"dpll_sound_{k}sat_n{n}_a{args.alpha}_B{B}"
     # resident waves of the persistent grid -> how busy the waves were (tail of the batch)
     kern, lds, per_cu = _capi.plan(n, m, m * k, k)
     resident = min(B, torch.cuda.get_device_properties(dev).multi_processor_count * per_cu)
-    # busy wave-time over resident wave-time of the timed region (both streams)
+    # busy wave-time over resident wave-time of the timed region (all streams)
     util = ticks / world / hz / (resident * elapsed)
-    pmc = load_pmc(workload)
+    st = _capi.split_stats(streams[last].cuda_stream) if not args.no_split else {"done": 0}
+    split_used = bool(st["done"])
+    pmc = load_profile("pmc_traffic.json", workload)
+    kname = dpll_kernel_name(n, m, k, split_used)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-            "kernel": KERNELS[kern], "kernel_ms": kernel_ms, "kernel_ms_hip_events": event_ms,
-            "algorithmic_bytes_per_launch": alg_bytes}
+            "kernel": kname, "kernel_ms": kernel_ms, "kernel_ms_hip_events": event_ms,
+            "kernel_ms_exclusive": union_ms / args.steps, "achieved_exclusive": ach_excl,
+            "frac_exclusive": ach_excl / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg_bytes,
+            "overlap": f"{NS} streams: launches overlap, so kernel_ms (launch span, = rocprofv3's kernel "
+                       f"duration) sums to {sum(span_ms) / args.steps:.1f} ms per step while some launch runs "
+                       f"{union_ms / args.steps:.1f} ms per step (kernel_ms_exclusive <= ms_per_step)"}
 
     if capped:
         desc = (f"node-capped batched DPLL (SOUND mode, <= {args.node_limit} calls per instance), random {k}-SAT "
@@ -490,10 +467,11 @@ def main():
                 f"n={n} alpha={args.alpha} m={m}, {args.total} instances per step sharded over "
                 f"{world} GPU(s) (BASELINE {args.config_name})")
     out = {
-        "metric": METRIC, "value": value, "unit": "unit-props/s" if capped else "instances/s", "n_gpus": world, "steps": args.steps,
-        "warmup": warm, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+        "metric": METRIC, "value": value, "unit": "unit-props/s" if capped else "instances/s", "n_gpus": world,
+        "steps": args.steps, "warmup": warm, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int32",
-        "data": f"synthetic: uniform random k-SAT generated in HBM (seeded), {NS} batches rotated on {NS} streams",
+        "data": f"synthetic: uniform random k-SAT generated in HBM (chunks of {CHUNK} seeded by chunk index: "
+                f"the same instances for every N), {NS} batches rotated on {NS} streams",
         "config": {"workload": desc, "preset": args.workload, "node_limit": args.node_limit,
                    "instances_per_step": args.total, "instances_per_gpu": B, "n": n, "m": m, "k": k,
                    "parallelism": f"instance-sharded x{world}", "streams": NS,
@@ -506,18 +484,253 @@ def main():
         "sat_fraction": nsat / all_inst,
         "hbm_gbs": achieved,
         "wave_utilisation": util,
+        "verdict_sha": verdict_sha, "n_ranks_seen": int(seen.item()),
+        "last_step_totals": {"sat": int((verdicts > 0).sum().item()), "nodes": int(ctr_tot[0].item()),
+                             "unit_props": int(ctr_tot[2].item())},
         "roofline": roof,
         "roofline_issue": issue_roofline(args.workload, B, kernel_ms),
+        "branch_split": st if split_used else None,   # None: the last launch did not split (auto policy)
     }
-    if not args.no_split:   # the last launch's branch-splitting statistics (satmi_dpll_split_stats)
-        st = _capi.split_stats(streams[(args.steps - 1) % NS].cuda_stream)
-        out["branch_split"] = st if st["done"] else None   # None: the launch did not split (auto policy)
+    host = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:
+        host = cnf.CnfBatch(icb.cpu().numpy(), clb.cpu().numpy(), lits.cpu().numpy(), nv.cpu().numpy())
+    return out, host
+
+
+def dp_roofline(stats, cus, clock_hz):
+    """Davis-Putnam (php-dp): the subsumption filter dominates (dp_subsume_tiled_kernel,
+    one lane per new clause, candidate keys broadcast from LDS).  Its binding
+    resource is the LDS issue pipe: one ds_read of a K-word key serves the 256
+    lanes of a workgroup, so a CU retires at most 64 / K subset tests per
+    cycle (64 lanes x one key word per LDS instruction per cycle).  achieved =
+    subset tests performed / the filter's device time (HIP events)."""
+    if not stats:
+        return None
+    tests = sum(s["subset_tests"] for s in stats) / len(stats)
+    ms = sum(s["subsume_ms"] for s in stats) / len(stats)
+    K = stats[-1]["words"]
+    if ms <= 0 or K <= 0:
+        return None
+    ach = tests / (ms * 1e-3)
+    peak = cus * clock_hz * 64.0 / K
+    return {"bound": "lds-issue", "achieved": ach, "peak": peak, "unit": "subset-tests/s", "frac": ach / peak,
+            "traffic": None, "kernel": "dp_subsume_tiled_kernel", "kernel_ms_per_step": ms,
+            "subset_tests_per_step": tests, "new_clauses_per_step": sum(s["new_clauses"] for s in stats) / len(stats),
+            "key_words": K, "clock_hz": clock_hz}
+
+
+def saturation_roofline(stats):
+    """Resolution (php-res): the dominant of its two kernels per step, timed by
+    HIP events on the library's stream (satmi_resolution_last_stats).  Claim
+    kernel (hash dedup): per candidate its key (8K B) read, one table slot
+    read + CAS (16 B), the occupant's key compared (8K B), flag + slot written
+    (16 B); pair kernel: per pair key i read (8K B), per candidate its key
+    written (8K B); K = 2 x 64-bit words per clause for <= 64 variables."""
+    if not stats:
+        return None
+    K = 2   # PHP(4,3): 12 variables -> one word per sign
+    cand = sum(s["candidates"] for s in stats) / len(stats)
+    pairs = sum(s["pairs"] for s in stats) / len(stats)
+    cms = sum(s["claim_ms"] for s in stats) / len(stats)
+    pms = sum(s["pair_ms"] for s in stats) / len(stats)
+    claim_b = cand * (16 * K + 32)
+    pair_b = pairs * 8 * K + cand * 8 * K
+    name, b, ms = ("ht_cand_kernel (hash claims)", claim_b, cms) if cms >= pms else \
+        ("res_pairs_kernel", pair_b, pms)
+    ach = b / (ms * 1e-3) / 1e9
+    pmc = load_profile("pmc_traffic.json", "php-res_" + name.split()[0])
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": pmc.get("hbm_bytes_per_step") if pmc else None, "kernel": name,
+            "kernel_ms_per_step": ms, "algorithmic_bytes_per_step": b,
+            "candidates_per_step": cand, "pairs_per_step": pairs, "pair_ms_per_step": pms, "claim_ms_per_step": cms}
+
+
+def run_saturation(args, world, rank, local):
+    """configs[3]: Davis-Putnam / resolution saturation of a pigeonhole formula.
+    A step = one full satmi_dp_host / satmi_resolution_host call (host arrays in,
+    verdict out: the boundary these solvers have, REF.py:63-130).  Each rank
+    solves its own replica (one formula does not shard)."""
+    from satmi.dp import eliminate
+    from satmi.dp import last_stats as dp_stats
+    from satmi.resolution import last_stats as res_stats
+    from satmi.resolution import resolve
+    torch.cuda.set_device(local)
+    holes, npass = SATURATION[args.workload]
+    f = cnf.pigeonhole(holes)
+    if args.workload == "php-dp":
+        run = lambda: eliminate(f)                                  # noqa: E731
+        work = lambda r: 1                                          # noqa: E731
+        unit, metric_desc = "solves/s", f"Davis-Putnam elimination of PHP({holes + 1},{holes})"
+    else:
+        run = lambda: resolve(f, max_passes=npass)                  # noqa: E731
+        work = lambda r: sum(r["pass_new"])                         # noqa: E731
+        unit, metric_desc = "derived clauses/s", f"resolution saturation of PHP({holes + 1},{holes}), first {npass} passes"
+    for _ in range(0 if args.profile_steps else args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    done = 0
+    last = None
+    stats = []
+    for _ in range(args.steps):
+        last = run()
+        done += work(last)
+        stats.append(res_stats() if args.workload == "php-res" else dp_stats())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    out = {"metric": METRIC, "value": done * world / elapsed, "unit": unit, "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic: pigeonhole formula",
+           "config": {"workload": metric_desc + " (BASELINE configs[3]); replicas across ranks",
+                      "preset": args.workload, "parallelism": f"replicas x{world}"},
+           "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
+           "roofline": saturation_roofline(stats) if args.workload == "php-res" else
+           dp_roofline(stats, torch.cuda.get_device_properties(local).multi_processor_count, SHADER_CLOCK_HZ)}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:
+        # the oracle on the same formula: checked against the GPU, then replicas
+        # on every host core (oracle/cpu_pool.py)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        r = oracle.dp(f) if args.workload == "php-dp" else oracle.resolution(f, max_passes=npass)
+        w = 1 if args.workload == "php-dp" else sum(r["pass_new"])
+        if r["result"] != last["result"] or w != work(last):
+            raise SystemExit("bench: GPU and oracle disagree on the configs[3] workload")
+        hb = cnf.pack([f])
+        pool, cores = cpu_pool("dp" if args.workload == "php-dp" else "res", hb.inst_clause_begin,
+                               hb.clause_lit_begin, hb.lits, args.cpu_seconds, npass)
+        cpu = {"value": pool["units_per_s"], "unit": unit, "cores": cores, "kind": "port",
+               "sample": f"{metric_desc} by the oracle (oracle/*.c) replicated on {cores} worker processes "
+                         f"(one per host core) for {pool['seconds']:.1f} s: {pool['units']} units",
+               "single_core_estimate": pool["units_per_s"] / cores}
+    out["cpu_baseline"] = cpu
+    return out
+
+
+def run_cdcl(args, world, rank, local):
+    """The reference's CDCLSolver (REF.py:217-384) batched on the GPU
+    (csrc/cdcl.hip, one wavefront per formula): a step = one satmi_cdcl_batch_host
+    call over the preset's formulas (host arrays in, verdicts out), each run to
+    its verdict or max_iter iterations (the reference's own loop is unbounded;
+    its driver times it out).  Replicas across ranks."""
+    import random
+
+    from satmi import solvers
+    from satmi.cdcl import CDCL_LIMIT, CDCL_SAT, CDCL_UNSAT, cdcl_batch_packed
+    torch.cuda.set_device(local)
+    nf, ncl, maxlit, nvar, max_iter, seed = CDCL[args.workload]
+    random.seed(seed)
+    formulas = [solvers.generate_large_formula(ncl, maxlit, nvar) for _ in range(nf)]
+    hb = cnf.pack(formulas)   # the CSR host arrays the C ABI takes, packed once
+    for _ in range(0 if args.profile_steps else args.warmup):
+        cdcl_batch_packed(hb, max_iter=max_iter)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = cdcl_batch_packed(hb, max_iter=max_iter)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    st = [r["status"] for r in res]
+    iters = sum(r["stats"]["iterations"] for r in res)
+    out = {"metric": METRIC, "value": nf * args.steps * world / elapsed, "unit": "formulas/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32/f64 activities",
+           "data": f"synthetic: {nf} x generate_large_formula({ncl}, {maxlit}, {nvar}) (REF.py:21-29, "
+                   f"random.seed({seed}))",
+           "config": {"workload": f"cdcl_solve (REF.py:382-384) on {nf} formulas, <= {max_iter} iterations each; "
+                                  f"replicas across ranks", "preset": args.workload,
+                      "parallelism": f"replicas x{world}"},
+           "sat": st.count(CDCL_SAT), "unsat": st.count(CDCL_UNSAT), "iteration_capped": st.count(CDCL_LIMIT),
+           "iterations_per_s": iters * args.steps * world / elapsed,
+           "roofline": None}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        for i in range(0, nf, max(1, nf // 16)):   # verdicts checked against the oracle on a sample
+            o = oracle.cdcl(formulas[i], max_iter=max_iter)
+            g = {CDCL_SAT: 1, CDCL_UNSAT: 0, CDCL_LIMIT: -1}.get(res[i]["status"], -2)
+            if o["result"] != g or (g == 1 and o["assignment"] != res[i]["assignment"]):
+                raise SystemExit(f"bench: GPU and oracle disagree on CDCL formula {i}")
+        pool, cores = cpu_pool("cdcl", hb.inst_clause_begin, hb.clause_lit_begin, hb.lits, args.cpu_seconds,
+                               max_iter)
+        cpu = {"value": pool["units_per_s"], "unit": "formulas/s", "cores": cores, "kind": "port",
+               "sample": f"{pool['units']} of the same formulas by oracle/cdcl_oracle.c on {cores} worker "
+                         f"processes (one per host core) for {pool['seconds']:.1f} s"}
+    out["cpu_baseline"] = cpu
+    return out
+
+
+def run_one(args, world, rank, local):
+    if args.workload in SATURATION:
+        return run_saturation(args, world, rank, local)
+    if args.workload in CDCL:
+        return run_cdcl(args, world, rank, local)
+    out, host = run_dpll(args, world, rank, local)
+    out["cpu_baseline"] = cpu_baseline(host, args.cpu_seconds, args.node_limit) if host is not None else None
+    return out
+
+
+def legs_main(args):
+    """The default run's child: every other BASELINE config, short, one JSON
+    object {name: compact line}.  A child process so that its 16-stream leg
+    gets a hardware queue per stream (GPU_MAX_HW_QUEUES, read at HIP start)."""
+    out = {}
+    for name, wl, extra in LEGS:
+        a = parse(["--workload", wl, "--cpu-seconds", str(args.leg_cpu_seconds), "--seed", str(args.seed)] + extra)
+        t = time.perf_counter()
+        r = run_one(a, 1, 0, 0)
+        keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_issue",
+                "cpu_baseline", "result", "passes_or_steps", "instances_per_s", "unit_props_per_s",
+                "capped_fraction", "sat_fraction", "sat", "unsat", "iteration_capped", "iterations_per_s",
+                "verdict_sha")
+        out[name] = {k: r[k] for k in keep if k in r}
+        out[name]["leg_wall_s"] = time.perf_counter() - t
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    args = parse()
+    if args.legs_only:
+        return legs_main(args)
+    world, rank, local = init_ranks()
+    if args.workload == "3sat-n50" and (args.streams or 16) > 3 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 17:
+        print("bench: note: GPU_MAX_HW_QUEUES < streams + 1, the streams share hardware queues", file=sys.stderr)
+    t_start = time.perf_counter()
+    out = run_one(args, world, rank, local)
+    legs = (world == 1 and not args.no_legs and not args.profile_steps and args.workload == "3sat-n100"
+            and args.total == WORKLOADS["3sat-n100"][0])
+    if legs and rank == 0:
+        env = dict(os.environ, GPU_MAX_HW_QUEUES="17")
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--legs-only", "--seed", str(args.seed),
+                            "--leg-cpu-seconds", str(args.leg_cpu_seconds)]
+                           + (["--no-cpu-baseline"] if args.no_cpu_baseline else []),
+                           capture_output=True, text=True, env=env)
+        if r.returncode != 0:
+            raise SystemExit(f"bench: secondary configs failed:\n{r.stderr[-4000:]}")
+        out["configs"] = json.loads(r.stdout.strip().splitlines()[-1])
+        out["configs_note"] = ("the other BASELINE configs, measured after the headline by a child process "
+                               "(bench.py --legs-only, GPU_MAX_HW_QUEUES=17) with the same harness; "
+                               "configs[1] reported on 2 streams (one batch of 4,096 in flight behind another) "
+                               "and on 16 streams (16 resident batches, ~65 k instances in flight)")
     if rank == 0:
-        if world == 1 and not args.no_cpu_baseline and not args.profile_steps:
-            host = cnf.CnfBatch(icb.cpu().numpy(), clb.cpu().numpy(), lits.cpu().numpy(), nv.cpu().numpy())
-            out["cpu_baseline"] = cpu_baseline(host, args.cpu_seconds, args.node_limit)
-        else:
-            out["cpu_baseline"] = None
+        out["wall_s"] = time.perf_counter() - t_start
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -248,10 +248,11 @@ int satmi_dpll_set_split(int enable, int helpers_per_cu);
  * search. */
 int satmi_dpll_set_split_warmup(int nodes);
 
-/* Branch-splitting statistics of the last split launch on `stream` (waits for
+/* Branch-splitting statistics of the last DPLL launch on `stream` (waits for
  * the stream): out[0..6] = donations, helper tickets, subtrees run by helpers,
  * donations taken back by their donors, waves that registered as helpers,
- * donors' ticks spent waiting on helpers, root instances finished. */
+ * donors' ticks spent waiting on helpers, root instances finished.  All zero
+ * (out[6] = 0) when that launch did not split. */
 int satmi_dpll_split_stats(void *stream, int64_t *out);
 
 /* The launch satmi_dpll_batch_device would make for this batch shape under the

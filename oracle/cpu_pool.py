@@ -1,19 +1,23 @@
-"""CPU baseline on all host cores: the oracle's SOUND-mode DPLL (oracle/sat_oracle.c,
-a C restatement of REF.py:133-214) over a sample of the bench batch, one worker
-process per core.
+"""CPU baselines on all host cores: the oracle (oracle/*.c, C restatements of
+REF.py's solvers) over a sample of a bench workload, one worker process per core.
 
-TEST INFRASTRUCTURE ONLY: bench.py's cpu_baseline leg runs this file as a CHILD
+TEST INFRASTRUCTURE ONLY: bench.py's cpu_baseline legs run this file as a CHILD
 PROCESS (it never imports torch and never touches the GPU), so the worker pool
 is forked from a process with no HIP state.
 
-    python oracle/cpu_pool.py <batch_dir> <seconds> <node_limit> <workers>
+    python oracle/cpu_pool.py <kind> <batch_dir> <seconds> <param> <workers>
 
 <batch_dir> holds icb.npy / clb.npy / lits.npy (the CSR arrays of include/satmi.h),
-memory-mapped by every worker.
-
-Worker w solves instances w, w + workers, w + 2*workers, ... of the sample until
-`seconds` pass; prints one JSON line: instances and unit-props per second over
-the slowest worker's wall time.
+memory-mapped by every worker.  Kinds:
+    dpll  SOUND-mode DPLL (REF.py:133-214), <param> = node limit (0: none);
+          worker w solves instances w, w + workers, ... of the sample
+    cdcl  cdcl_solve (REF.py:217-384), <param> = max_iter; instances as dpll
+    dp    Davis-Putnam (REF.py:98-130) of instance 0, repeated (replicas)
+    res   resolution (REF.py:63-95) of instance 0, <param> = passes, repeated;
+          the unit is derived clauses
+until `seconds` pass (every worker finishes at least one unit).  Prints one
+JSON line: units and unit-props (dpll) per second over the slowest worker's
+wall time.
 """
 import json
 import multiprocessing as mp
@@ -32,34 +36,55 @@ def _instance(icb, clb, lits, b):
     return [lits[clb[c]:clb[c + 1]].tolist() for c in range(c0, c1)]
 
 
+def _solve(kind, f, param):
+    """(units, unit-props) of one oracle call."""
+    if kind == "dpll":
+        r = oracle.dpll(f, "sound", max_solutions=1, sol_cap=1, node_limit=param)
+        return 1, r["counters"]["unit_props"]
+    if kind == "cdcl":
+        oracle.cdcl(f, max_iter=param)
+        return 1, 0
+    if kind == "dp":
+        oracle.dp(f)
+        return 1, 0
+    if kind == "res":
+        return sum(oracle.resolution(f, max_passes=param)["pass_new"]), 0
+    raise ValueError(kind)
+
+
 def _worker(args):
-    path, seconds, node_limit, w, workers = args
+    kind, path, seconds, param, w, workers = args
     icb, clb, lits = (np.load(os.path.join(path, f + ".npy"), mmap_mode="r") for f in ("icb", "clb", "lits"))
     B = icb.shape[0] - 1
     oracle.lib()
     t0 = time.perf_counter()
     done = props = 0
-    for b in range(w, B, workers):
-        r = oracle.dpll(_instance(icb, clb, lits, b), "sound", max_solutions=1, sol_cap=1, node_limit=node_limit)
-        props += r["counters"]["unit_props"]
-        done += 1
+    replicas = kind in ("dp", "res")
+    f0 = _instance(icb, clb, lits, 0) if replicas else None
+    b = w
+    while replicas or b < B:
+        u, p = _solve(kind, f0 if replicas else _instance(icb, clb, lits, b), param)
+        done += u
+        props += p
+        b += workers
         if time.perf_counter() - t0 > seconds:
             break
     return done, props, time.perf_counter() - t0
 
 
-def run(path, seconds, node_limit, workers):
+def run(kind, path, seconds, param, workers):
     oracle.lib()   # build once before forking
     ctx = mp.get_context("fork")
     with ctx.Pool(workers) as pool:
-        res = pool.map(_worker, [(path, seconds, node_limit, w, workers) for w in range(workers)])
+        res = pool.map(_worker, [(kind, path, seconds, param, w, workers) for w in range(workers)])
     done = sum(r[0] for r in res)
     props = sum(r[1] for r in res)
     wall = max(r[2] for r in res)
-    return {"instances": done, "unit_props": props, "seconds": wall, "workers": workers,
-            "instances_per_s": done / wall, "unit_props_per_s": props / wall}
+    return {"kind": kind, "units": done, "instances": done, "unit_props": props, "seconds": wall,
+            "workers": workers, "units_per_s": done / wall, "instances_per_s": done / wall,
+            "unit_props_per_s": props / wall}
 
 
 if __name__ == "__main__":
-    p, s, nl, wk = sys.argv[1], float(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
-    print(json.dumps(run(p, s, nl, wk)), flush=True)
+    k, p, s, prm, wk = sys.argv[1], sys.argv[2], float(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+    print(json.dumps(run(k, p, s, prm, wk)), flush=True)

@@ -52,6 +52,7 @@ struct CdclLayout {
         slot, scratch, bytes;
     int64_t clause_cap, lit_cap, pool_cap, snap_cap;
     int32_t ncap;   // variables
+    int32_t lcap;   // one learned-literal list in scratch: 2 x variables + the longest clause (repeats)
 };
 
 struct CdclArgs {
@@ -323,11 +324,15 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
 
 // analyze_conflict (REF.py:306-345) on lane 0: learned literals into S.scratch
 // (returns their count), the backtrack level into *bt; -1 where the reference
-// raises KeyError (an unassigned variable reaching self.levels[...]).
+// raises KeyError (an unassigned variable reaching self.levels[...]); -2 if a
+// list would pass `cap` entries (the arena is full: CD_FULL).  A list holds
+// distinct literals plus the repeats of the conflict clause, so cap = 2 x
+// variables + the longest clause is never reached.
 __device__ int analyze_conflict(const St &S, int64_t conflict, int32_t cap, int32_t *bt) {
     const int64_t jb = S.coff[conflict], je = S.coff[conflict + 1];
     int32_t *L = S.scratch;
     int n = 0;
+    if (je - jb > cap) return -2;
     for (int64_t j = jb; j < je; ++j) {
         if (S.val[iabs(S.lits[j])] < 0) return -1;
         L[n++] = S.lits[j];
@@ -369,13 +374,16 @@ __device__ int analyze_conflict(const St &S, int64_t conflict, int32_t cap, int3
         for (int i = 0; i < n; ++i) {
             bool neg_in = false;
             for (int64_t j = ab; j < ae; ++j) neg_in |= S.lits[j] == -L[i];
-            if (L[i] != last && !neg_in) N[m++] = L[i];
+            if (L[i] != last && !neg_in) N[m++] = L[i];   // m <= n <= cap
         }
         for (int64_t j = ab; j < ae; ++j) {
             const int x = S.lits[j];
             bool in_new = false;
             for (int i = 0; i < m; ++i) in_new |= N[i] == x;
-            if (x != -last && !in_new && m < cap) N[m++] = x;
+            if (x != -last && !in_new) {
+                if (m >= cap) return -2;
+                N[m++] = x;
+            }
         }
         for (int i = 0; i < m; ++i) {
             if (S.val[iabs(N[i])] < 0) return -1;
@@ -465,7 +473,7 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
             ++conflicts;
             int32_t cnt = 0, bt = 0;
             if (ln == 0) {
-                cnt = analyze_conflict(S, conflict, A.lay.ncap * 2 + 2, &bt);
+                cnt = analyze_conflict(S, conflict, A.lay.lcap, &bt);
                 if (cnt > 0) {   // learn_clause (REF.py:347-357)
                     if (q.nf + 1 > A.lay.clause_cap || q.nlits + cnt > A.lay.lit_cap) {
                         q.full = true;
@@ -487,7 +495,8 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
             sync_seq(q);
             cnt = __builtin_amdgcn_readfirstlane(cnt);
             bt = __builtin_amdgcn_readfirstlane(bt);
-            if (cnt < 0) {
+            if (cnt == -2) q.full = true;   // scratch list bound (see analyze_conflict)
+            else if (cnt < 0) {
                 status = CD_ERROR;
                 break;
             }
@@ -635,7 +644,8 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     L->snap = o;    o = a(o + 4 * (uint64_t)SN);
     L->rep = o;     o = a(o + 4 * (uint64_t)SN);
     L->slot = o;    o = a(o + 4 * (uint64_t)SN);
-    L->scratch = o; o = a(o + 4 * (uint64_t)(4 * N + 8));   // two learned-literal lists of <= 2N
+    L->lcap = (int32_t)std::min<int64_t>(2 * N + 2 + std::max(max_len, 1), INT32_MAX / 8);
+    L->scratch = o; o = a(o + 4 * 2 * (uint64_t)L->lcap);   // two learned-literal lists
     L->bytes = o;
     L->clause_cap = C;
     L->lit_cap = Lc;

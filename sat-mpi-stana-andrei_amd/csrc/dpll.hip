@@ -1006,6 +1006,7 @@ struct DeviceWork {
     // shrunk) and the stream's launch tag for the slot states
     std::unordered_map<hipStream_t, std::pair<void *, size_t>> split;
     std::unordered_map<hipStream_t, uint32_t> split_epoch;
+    std::unordered_map<hipStream_t, bool> split_last;   // the stream's last DPLL launch split (stats valid)
     // wide general kernel: per-wave HBM arenas per stream (grown, never shrunk)
     std::unordered_map<hipStream_t, std::pair<void *, size_t>> arena;
     double ticks_per_s = 1e8;
@@ -1140,7 +1141,18 @@ static void *split_scratch(hipStream_t stream, size_t bytes, uint32_t *epoch) {
     ep = (ep + 1u) & 0x0FFFFFFFu;
     if (ep == 0u) ep = 1u;
     *epoch = ep;
+    g_work[dev].split_last[stream] = true;
     return slot.first;
+}
+
+// A DPLL launch on `stream` is about to be made: until its split_scratch call
+// (only launches that split make one) the stream has no split statistics.
+static void split_mark_unsplit(hipStream_t stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_work_mu);
+    if ((int)g_work.size() <= dev) g_work.resize(dev + 1);
+    g_work[dev].split_last[stream] = false;
 }
 
 extern "C" int satmi_dpll_split_stats(void *stream, int64_t *out) {
@@ -1156,10 +1168,12 @@ extern "C" int satmi_dpll_split_stats(void *stream, int64_t *out) {
         std::lock_guard<std::mutex> lk(g_work_mu);
         if ((int)g_work.size() > dev) {
             auto it = g_work[dev].split.find((hipStream_t)stream);
-            if (it != g_work[dev].split.end()) head = it->second.first;
+            auto last = g_work[dev].split_last.find((hipStream_t)stream);
+            if (it != g_work[dev].split.end() && last != g_work[dev].split_last.end() && last->second)
+                head = it->second.first;
         }
     }
-    if (!head) return SATMI_OK;   // no split launch on this stream yet
+    if (!head) return SATMI_OK;   // the stream's last launch did not split: all zero (done = 0)
     unsigned char h[SPLIT_HEAD_BYTES];
     SATMI_HIP(hipStreamSynchronize((hipStream_t)stream));
     SATMI_HIP(hipMemcpy(h, head, sizeof(h), hipMemcpyDeviceToHost));
@@ -1330,6 +1344,7 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
             return split_scratch((hipStream_t)stream, bytes, epoch);
         };
         SATMI_HIP(hipMemsetAsync(wc, 0, 24, Lc.stream));   // counter + launch span (common.h)
+        split_mark_unsplit(Lc.stream);
         return dpll_scan_launch(Lc);
     }
     DpllLayout lay;

@@ -74,6 +74,20 @@ enum { PH_STAGE = 0, PH_ASSIGN = 1, PH_UNITS = 2, PH_CONFLICT = 3, PH_COUNTS = 4
 
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 
+// Attribution builds only (`make variant VFLAGS=-DSATMI_DUP_<KIND>`, never the
+// product): every LDS access of one kind is issued a second time with an
+// effect-free operand (OR / ADD of an opaque zero, MIN of all ones, MAX of 0),
+// so the search is unchanged and the rise of SQ_LDS_BANK_CONFLICT over the
+// plain build is that kind's conflict cycles.  Kinds: GATHER (literal-state
+// byte gathers), CNT (counting-pass atomics), TS (snapshot stamp atomics),
+// CLS (touched-clause word reads of the incremental rounds), ASSIGN (the
+// batch assignment's stamp reads and state stores).
+__device__ __forceinline__ uint32_t opaque_zero() {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+
 // Literal state byte lv[code] (code = v << 1 | negative): free 1, true 8,
 // false 0.  The sum of a clause's bytes: bits 0-2 = free occurrences (REF.py's
 // len(c)), bits 3-7 = 8 x true occurrences (!= 0: the reference dropped the
@@ -169,6 +183,31 @@ __device__ __forceinline__ void lv_clear(uint8_t *lv, uint32_t v) {
 }
 __device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return (lv[2 * v] & 1u) != 0u; }
 
+// The hot LDS accesses by kind (see SATMI_DUP_* above).
+template <int K, typename C>
+__device__ __forceinline__ uint32_t lv_get(const SLds<K, C> &S, uint32_t code) {
+    uint32_t x = S.lv[code];
+#ifdef SATMI_DUP_GATHER
+    x |= (uint32_t)((const volatile uint8_t *)S.lv)[code] & opaque_zero();
+#endif
+    return x;
+}
+template <int K, typename C>
+__device__ __forceinline__ void ts_stamp(const SLds<K, C> &S, uint32_t v, uint32_t st) {
+    atomicMax(&S.ts[v], st);
+#ifdef SATMI_DUP_TS
+    atomicMax(&S.ts[v], st & opaque_zero());
+#endif
+}
+template <int K, typename C>
+__device__ __forceinline__ typename Pack<K>::W cls_at(const SLds<K, C> &S, uint32_t c) {
+    typename Pack<K>::W w = S.cls[c];
+#ifdef SATMI_DUP_CLS
+    w |= ((const volatile typename Pack<K>::W *)S.cls)[c] & (typename Pack<K>::W)opaque_zero();
+#endif
+    return w;
+}
+
 // Apply f(c, w, x) to every clause c (w its packed word, x[j] the state byte of
 // its slot j), one 64-clause chunk per lane step; the loads of U chunks are
 // issued before any is used.  mpad is a multiple of 64 (dummy clauses are
@@ -184,7 +223,7 @@ __device__ __forceinline__ void chunk_group(const SLds<K, C> &S, int c0, F &&f) 
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[u][j] = S.lv[field<K>(w[u], j)];
+        for (int j = 0; j < K; ++j) x[u][j] = lv_get(S, field<K>(w[u], j));
 #pragma unroll
     for (int u = 0; u < U; ++u) f(c0 + 64 * u + ln, w[u], x[u]);
 }
@@ -203,7 +242,7 @@ __device__ __forceinline__ void for_chunks(const SLds<K, C> &S, int mpad, F &&f)
         const W w = S.cls[c0 + ln];
         uint32_t x[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = S.lv[field<K>(w, j)];
+        for (int j = 0; j < K; ++j) x[j] = lv_get(S, field<K>(w, j));
         f(c0 + ln, w, x);
     }
 }
@@ -268,7 +307,7 @@ __device__ int scan_units(const SLds<K, C> &S, int mpad, uint32_t ep, uint32_t b
             const uint32_t k = (uint32_t)nu + (uint32_t)__popcll(mk & lt);
             const uint32_t code = unit_code<K>(S.cls[c], x);   // re-read: keeps U words out of VGPRs
             S.snap[k] = (C)code;
-            atomicMax(&S.ts[code >> 1], stamp(ep, k));
+            ts_stamp(S, code >> 1, stamp(ep, k));
         }
         nu += __popcll(mk);
     });
@@ -334,10 +373,10 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             }
             const bool valid = ln < total;
             const uint32_t c = S.occ[valid ? d + ln : 0];
-            const W w = S.cls[c];
+            const W w = cls_at(S, c);
             uint32_t x[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = S.lv[field<K>(w, j)];
+            for (int j = 0; j < K; ++j) x[j] = lv_get(S, field<K>(w, j));
             const uint32_t s = clause_sum<K>(x);
             const bool open = valid && !sum_true(s);
             const uint32_t nf = sum_nfree(s);
@@ -377,7 +416,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 if (unit && !dup) {
                     const uint32_t code = unit_code<K>(w, x);
                     S.snap[rank] = (C)code;
-                    atomicMax(&S.ts[code >> 1], stamp(ep, (uint32_t)rank));
+                    ts_stamp(S, code >> 1, stamp(ep, (uint32_t)rank));
                 }
                 wave_sync();
                 return __popcll(dm);
@@ -413,10 +452,10 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             ++passes;
             if (t < total) {
                 const uint32_t c = S.occ[d + t];
-                const W w = S.cls[c];
+                const W w = cls_at(S, c);
                 uint32_t x[K];
 #pragma unroll
-                for (int j = 0; j < K; ++j) x[j] = S.lv[field<K>(w, j)];
+                for (int j = 0; j < K; ++j) x[j] = lv_get(S, field<K>(w, j));
                 const uint32_t s = clause_sum<K>(x);
                 if (!sum_true(s)) {
                     const uint32_t nf = sum_nfree(s);
@@ -457,7 +496,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const uint2 p = S.bm[uc >> 5];
             const uint32_t k = p.y + (uint32_t)__popc(p.x & ((1u << (uc & 31u)) - 1u));
             S.snap[k] = (C)ucode;
-            atomicMax(&S.ts[ucode >> 1], stamp(ep, k));
+            ts_stamp(S, ucode >> 1, stamp(ep, k));
         }
     } else {
         // long batch: walk the bitmap word by word, re-deriving each unit literal
@@ -470,10 +509,10 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 const W wd = S.cls[c];
                 uint32_t x[K];
 #pragma unroll
-                for (int j = 0; j < K; ++j) x[j] = S.lv[field<K>(wd, j)];
+                for (int j = 0; j < K; ++j) x[j] = lv_get(S, field<K>(wd, j));
                 const uint32_t code = unit_code<K>(wd, x);
                 S.snap[k] = (C)code;
-                atomicMax(&S.ts[code >> 1], stamp(ep, k));
+                ts_stamp(S, code >> 1, stamp(ep, k));
                 ++k;
             }
         }
@@ -515,7 +554,12 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             const bool valid = k < nu;
             const uint32_t code = (uint32_t)S.snap[valid ? k : 0];   // predicated loads
             const uint32_t v = code >> 1;
+#ifdef SATMI_DUP_ASSIGN
+            const bool first = valid & (S.ts[v] == stamp(bep, (uint32_t)k)) &
+                               ((((const volatile uint32_t *)S.ts)[v] & opaque_zero()) == 0u);
+#else
             const bool first = valid & (S.ts[v] == stamp(bep, (uint32_t)k));
+#endif
             const uint64_t mk = __ballot(first);
             // predicated stores (no exec-mask branch): the other lanes write
             // the first entry past the batch (dead: the trail is a stack, and
@@ -523,6 +567,12 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             // padding / dummy codes' fixed states
             S.trail[tl + __popcll(mk & (first ? lt : ~0ull))] = (C)code;
             lv_assign(S.lv, first ? code : CODE_DUMMY);
+#ifdef SATMI_DUP_ASSIGN
+            {
+                const uint32_t cd = first ? code : CODE_DUMMY;
+                *(volatile uint16_t *)(S.lv + (cd & ~1u)) = (uint16_t)((cd & 1u) ? (LV_TRUE << 8) : LV_TRUE);
+            }
+#endif
             tl += __popcll(mk);
             k0 += 64;
         } while (k0 < nu);
@@ -557,16 +607,19 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
 }
 
 // literal_sign / var_counts scan (REF.py:174-179, :198-203): every free
-// occurrence in an active clause is counted per variable, and the first
-// position kept.  Returns whether any clause is active (none: REF.py:170-171).
-// Within an active clause the atomics run for every slot -- a falsified slot
-// adds 0 / mins NONE32, padding hits variable 0 (never read) -- so there is
-// no branch per slot.
+// occurrence in an active clause is counted per variable.  Returns whether
+// any clause is active (none: REF.py:170-171).  Within an active clause the
+// atomic runs for every slot -- a falsified slot adds 0, padding hits
+// variable 0 (never read) -- so there is no branch per slot.  The dict order
+// (first positions) is not tracked here: only the branch candidates and the
+// pure literals need it, and choose() finds those afterwards (a per-slot
+// atomicMin of the first position here cost 21 LDS atomics per node, most of
+// the kernel's bank-conflict cycles).
 template <int K, typename C>
 __device__ int scan_counts(const SLds<K, C> &S, int mpad) {
     using W = typename Pack<K>::W;
     uint64_t any = 0;   // only "no active clause" matters: OR the ballots (one scalar op per chunk)
-    for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int c, W w, const uint32_t(&x)[K]) {
+    for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int, W w, const uint32_t(&x)[K]) {
         const bool act = !sum_true(clause_sum<K>(x));
         any |= __ballot(act);
         if (act) {
@@ -575,12 +628,73 @@ __device__ int scan_counts(const SLds<K, C> &S, int mpad) {
                 const uint32_t code = field<K>(w, j);
                 const bool fr = (x[j] & 1u) != 0u;
                 atomicAdd(&S.cnt[code >> 1], fr ? ((code & 1u) ? 0x10000u : 1u) : 0u);
-                atomicMin(&S.first[code >> 1], fr ? (((uint32_t)c << 3) | (uint32_t)j) : NONE32);
+#ifdef SATMI_DUP_CNT
+                atomicAdd(&S.cnt[code >> 1], opaque_zero());
+#endif
             }
         }
     });
     wave_sync();
     return any != 0ull;
+}
+
+// Positions in the reduced formula: c << 3 | slot, in REF.py's iteration
+// order (clauses in order, literals in order), over the free literals of the
+// active clauses.  S.first[v] != 0 flags variable v for the two scans below.
+//
+// The first flagged position (chunks in order, the scan stops at the first
+// chunk with a hit): the first flagged key in dict order.
+template <int K, typename C>
+__device__ uint32_t first_flagged(const SLds<K, C> &S, int mpad) {
+    using W = typename Pack<K>::W;
+    const int ln = lane_id();
+    for (int c0 = 0; c0 < mpad; c0 += 64) {
+        const int c = c0 + ln;
+        const W w = S.cls[c];
+        uint32_t x[K], f[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            x[j] = lv_get(S, field<K>(w, j));
+            f[j] = S.first[field<K>(w, j) >> 1];
+        }
+        const bool act = !sum_true(clause_sum<K>(x));
+        uint32_t pos = NONE32;
+#pragma unroll
+        for (int j = K - 1; j >= 0; --j)
+            pos = act & ((x[j] & 1u) != 0u) & (f[j] != 0u) ? (((uint32_t)c << 3) | (uint32_t)j) : pos;
+        const uint64_t hit = __ballot(pos != NONE32);
+        if (hit) return (uint32_t)__builtin_amdgcn_readlane((int)pos, __builtin_ctzll(hit));
+    }
+    return NONE32;   // unreachable: a flagged variable occurs free in an active clause
+}
+
+// First positions of the `npure` flagged (pure) variables: S.first[v] = its
+// first position + 1 (flag NONE32 before; 0 = not pure).  Chunks in order
+// until every pure variable has been met once.
+template <int K, typename C>
+__device__ void first_of_pures(const SLds<K, C> &S, int mpad, int npure) {
+    using W = typename Pack<K>::W;
+    const int ln = lane_id();
+    int found = 0;
+    for (int c0 = 0; c0 < mpad && found < npure; c0 += 64) {
+        const int c = c0 + ln;
+        const W w = S.cls[c];
+        uint32_t x[K], f[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            x[j] = lv_get(S, field<K>(w, j));
+            f[j] = S.first[field<K>(w, j) >> 1];
+        }
+        const bool act = !sum_true(clause_sum<K>(x));
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            bool met = false;
+            if (act & ((x[j] & 1u) != 0u) & (f[j] != 0u))
+                met = atomicMin(&S.first[field<K>(w, j) >> 1], (((uint32_t)c << 3) | (uint32_t)j) + 1u) == NONE32;
+            found += __popcll(__ballot(met));
+        }
+    }
+    wave_sync();
 }
 
 struct Choice {
@@ -590,49 +704,90 @@ struct Choice {
 
 // pure_literals (REF.py:181-184) into plist (first positions), else the
 // branching variable: max(var_counts.items(), key=count), the first maximal
-// key in dict order (REF.py:208).  Clears cnt / first for the next scan.
+// key in dict order (REF.py:208).  Clears cnt for the next scan.  The
+// variables are read twice -- the largest count and the pure count, then the
+// flags of the position scans -- and a position scan runs only when the
+// order matters: several variables share the largest count (the first of
+// them in dict order wins), or there are pure literals (their order is the
+// assignment's dict order).
 template <int K, typename C>
-__device__ Choice choose(const SLds<K, C> &S, int n) {
+__device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     int npure = 0;
-    // per lane: its largest count and, among its variables with that count,
-    // the smallest first position (one pass; the wave's winner is the smallest
-    // first position among the lanes holding the wave's largest count)
-    uint32_t lmax = 0, lbest = NONE32;
+    uint32_t lmax = 0;
     // predicated (no exec-mask branches): lanes past n read variable n's words
-    auto step = [&](int v0) {
+    auto count_step = [&](int v0) {
         const int v = v0 + ln;
         const uint32_t vc = (uint32_t)min(v, n);
         const bool live = (v <= n) & var_free(S.lv, vc);
         const uint32_t c = S.cnt[vc];
         const uint32_t p = c & 0xFFFFu, q = c >> 16;
-        const uint32_t f = S.first[vc];
-        S.cnt[vc] = 0u;   // cleared for the next scan as soon as read
-        S.first[vc] = NONE32;
-        const bool better = live & ((p + q > lmax) | ((p + q == lmax) & (f < lbest)));
-        lmax = better ? p + q : lmax;
-        lbest = better ? f : lbest;
-        const bool pure = live & ((p + q) != 0u) & ((p == 0u) | (q == 0u));
-        const uint64_t mk = __ballot(pure);
-        if (pure) S.plist[npure + __popcll(mk & lt)] = f;
-        npure += __popcll(mk);
+        lmax = live ? max(lmax, p + q) : lmax;
+        npure += __popcll(__ballot(live & ((p + q) != 0u) & ((p == 0u) | (q == 0u))));
     };
     if constexpr (sizeof(C) == 1) {   // byte trail codes: n <= 127, two steps at most, no loop
-        if (n >= 1) step(1);
-        if (n >= 65) step(65);
+        if (n >= 1) count_step(1);
+        if (n >= 65) count_step(65);
     } else {
-        for (int v0 = 1; v0 <= n; v0 += 64) step(v0);
+        for (int v0 = 1; v0 <= n; v0 += 64) count_step(v0);
     }
     const uint32_t maxc = wave_max_u32(lmax);
-    uint32_t best = 0;
-    if (npure == 0 && maxc > 0) {
-        const uint32_t bestf = wave_min_u32(lmax == maxc ? lbest : NONE32);
-        best = uniform_u32(field<K>(S.cls[bestf >> 3], (int)(bestf & 7u)) >> 1);
+    int ncand = 0;
+    uint32_t cvar = 0;   // the first candidate by variable index (the winner when it is the only one)
+    // flags for the position scans (lanes past n flag variable 0: never flagged), counts cleared
+    auto flag_step = [&](int v0) {
+        const int v = v0 + ln;
+        const uint32_t vc = (uint32_t)min(v, n);
+        const bool live = (v <= n) & var_free(S.lv, vc);
+        const uint32_t c = S.cnt[vc];
+        const uint32_t p = c & 0xFFFFu, q = c >> 16;
+        const bool pure = live & ((p + q) != 0u) & ((p == 0u) | (q == 0u));
+        const bool cand = live & (p + q == maxc);
+        const uint64_t cm = __ballot(cand);
+        cvar = (ncand == 0 && cm) ? (uint32_t)v0 + (uint32_t)__builtin_ctzll(cm) : cvar;
+        ncand += __popcll(cm);
+        const uint32_t vw = v <= n ? vc : 0u;
+        S.first[vw] = npure ? (pure ? NONE32 : 0u) : (cand ? 1u : 0u);
+        S.cnt[vw] = 0u;   // cleared for the next scan
+    };
+    if constexpr (sizeof(C) == 1) {
+        if (n >= 1) flag_step(1);
+        if (n >= 65) flag_step(65);
+    } else {
+        for (int v0 = 1; v0 <= n; v0 += 64) flag_step(v0);
     }
     S.cnt[0] = 0u;   // variable 0: the padding slots' counts (never read)
-    S.first[0] = NONE32;
+    S.first[0] = 0u;
     wave_sync();
+    uint32_t best = 0;
+    if (npure > 0) {
+        first_of_pures<K>(S, mpad, npure);
+        // plist in variable order; assign_pures ranks the entries by position
+        int k = 0;
+        auto collect = [&](int v0) {
+            const int v = v0 + ln;
+            const uint32_t f = v <= n ? S.first[v] : 0u;
+            const bool pure = f != 0u;
+            const uint64_t mk = __ballot(pure);
+            if (pure) S.plist[k + __popcll(mk & lt)] = f - 1u;
+            k += __popcll(mk);
+        };
+        if constexpr (sizeof(C) == 1) {
+            if (n >= 1) collect(1);
+            if (n >= 65) collect(65);
+        } else {
+            for (int v0 = 1; v0 <= n; v0 += 64) collect(v0);
+        }
+        wave_sync();
+    } else if (maxc > 0) {
+        if (ncand == 1) {
+            best = cvar;
+        } else {
+            const uint32_t bestf = first_flagged<K>(S, mpad);
+            best = uniform_u32(field<K>(S.cls[bestf >> 3], (int)(bestf & 7u)) >> 1);
+        }
+    }
     return {npure, best};
 }
 
@@ -1123,7 +1278,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
             if (nact == 0) {
                 leaf = true;                                   // REF.py:170-171
             } else {
-                r = choose<K>(S, n);
+                r = choose<K>(S, n, mpad);
                 if (r.npure == 0 && r.best_var == 0u) leaf = true;   // REF.py:205-206
             }
             ph.mark(PH_CHOOSE);

@@ -164,10 +164,15 @@ __global__ void __launch_bounds__(256) res_pairs_kernel(const uint64_t *keys, in
                 pos = uniform_i32(pos) + __popcll(m & lanemask_lt());
                 if (cls == 1) ibuf[pos] = (int32_t)i;
             }
+            // block-uniform flush decision: every wave reads the settled count
+            // before any wave can append again (a second barrier), and the
+            // last step of j flushes whatever is buffered
             __syncthreads();
-            if (nbuf > PAIR_BUF - (int)blockDim.x) flush();
+            const int nb = nbuf;
+            __syncthreads();
+            const bool last = i0 + (int64_t)blockDim.x >= j;
+            if (nb > (last ? 0 : PAIR_BUF - (int)blockDim.x)) flush();
         }
-        if (nbuf > 0) flush();
     }
 }
 
@@ -259,12 +264,21 @@ struct DevBuf {
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
+    // grow to `bytes` (contents not kept); SATMI_ERR_NOMEM with a hint when the
+    // device cannot hold it
     int reserve(size_t bytes) {
         if (bytes <= cap) return SATMI_OK;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
         const size_t want = std::max(bytes, (size_t)256);
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && want > free_b) {
+            set_error("satmi_resolution_host: out of device memory (" + std::to_string(want >> 20) + " MiB wanted, " +
+                      std::to_string(free_b >> 20) + " MiB free); bound the saturation with clause_limit / "
+                      "max_passes");
+            return SATMI_ERR_NOMEM;
+        }
         SATMI_HIP(hipMalloc(&p, want));
         cap = want;
         return SATMI_OK;
@@ -285,10 +299,13 @@ uint64_t table_slots(int64_t keys) {
     return cap;
 }
 
-// Pairs per chunk of a pass: the candidate buffer holds one chunk's worst
-// case (every pair a candidate), so a chunk never overflows; the deadline is
-// checked between chunks, so a long pass ends as a timeout (REF.py:417-437).
+// Pairs per chunk of a pass (the deadline is checked between chunks, so a long
+// pass ends as a timeout, REF.py:417-437).  The candidate buffer holds a
+// chunk's worst case (every pair a candidate) up to CAND_BYTES; past that it
+// starts at CAND_BYTES, and a chunk whose candidates overflow it is re-run
+// once with a buffer of the counted size.
 constexpr int64_t PAIR_CHUNK = 1ll << 27;
+constexpr size_t CAND_BYTES = (size_t)1 << 30;
 
 int64_t g_slot_base = 0;   // test knob: first append slot of the pair kernel
 
@@ -484,21 +501,28 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
             int64_t j1 = (int64_t)(0.5 + std::sqrt(0.25 + 2.0 * t1));
             j1 = std::min(ncl, std::max(j1, j0 + 1));
             while (j1 > j0 + 1 && (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2 > PAIR_CHUNK) --j1;
-            const int64_t cap = std::max<int64_t>(1, (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2);
-            SATMI_TRY(cand.reserve(8 * (size_t)cap * K));
+            const int64_t npairs = std::max<int64_t>(1, (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2);
+            SATMI_TRY(cand.reserve(std::min(8 * (size_t)npairs * K, std::max(CAND_BYTES, cand.cap))));
             struct {
                 unsigned long long count;
                 int empty;
                 int pad;
             } hc{(unsigned long long)slot_base, 0, 0};
-            SATMI_HIP(hipMemcpyAsync(counters.p, &hc, 16, hipMemcpyHostToDevice, s));
-            t_pairs.begin(s);
-            launch_pairs(j0, j1, cap);
-            t_pairs.end(s);
-            g_stats.pairs += (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2;
-            SATMI_HIP(hipGetLastError());
-            SATMI_HIP(hipMemcpyAsync(&hc, counters.p, 16, hipMemcpyDeviceToHost, s));
-            SATMI_HIP(hipStreamSynchronize(s));
+            for (int attempt = 0;; ++attempt) {
+                const int64_t cap = (int64_t)(cand.cap / (8 * (size_t)K));
+                hc = {(unsigned long long)slot_base, 0, 0};
+                SATMI_HIP(hipMemcpyAsync(counters.p, &hc, 16, hipMemcpyHostToDevice, s));
+                t_pairs.begin(s);
+                launch_pairs(j0, j1, cap);
+                t_pairs.end(s);
+                SATMI_HIP(hipGetLastError());
+                SATMI_HIP(hipMemcpyAsync(&hc, counters.p, 16, hipMemcpyDeviceToHost, s));
+                SATMI_HIP(hipStreamSynchronize(s));
+                const int64_t counted = (int64_t)(hc.count - (unsigned long long)slot_base);
+                if (hc.empty || counted <= cap || attempt > 0) break;
+                SATMI_TRY(cand.reserve(8 * (size_t)counted * K));   // overflowed: re-run at the counted size
+            }
+            g_stats.pairs += npairs;
             j0 = j1;
             if (hc.empty) {   // an empty resolvent: unsatisfiable (REF.py:84-85)
                 empty = true;

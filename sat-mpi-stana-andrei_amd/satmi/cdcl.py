@@ -25,9 +25,13 @@ class CdclLimit(Exception):
 def cdcl_batch(formulas, max_iter=0, time_limit=0.0, learn_cap=0):
     """Run cdcl_solve on every formula.  Returns a list of dicts: status
     (CDCL_*), assignment (signed literals, dict order), stats, var_inc."""
+    return cdcl_batch_packed(pack(formulas), max_iter=max_iter, time_limit=time_limit, learn_cap=learn_cap)
+
+
+def cdcl_batch_packed(batch, max_iter=0, time_limit=0.0, learn_cap=0):
+    """cdcl_batch on a CnfBatch (the CSR host arrays of include/satmi.h)."""
     L = _capi.load()
     _capi.require_gpu()
-    batch = pack(formulas)
     B = batch.num_instances
     nv = max([int(batch.inst_nvars.max()) if B else 0, 1])
     status = np.zeros(B, dtype=np.int32)

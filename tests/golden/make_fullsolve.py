@@ -1,8 +1,12 @@
-"""Fixtures for configs[4] solved to completion (no node cap): uf250-shaped
-random 3-SAT (n=250, m=1065), SOUND mode, first model.
-
-Run here (CPU, ~30 min on 8 cores):
-    python tests/golden/make_fullsolve.py
+"""Fixtures for configs[4] solved to completion (no node cap), SOUND mode,
+first model:
+    uf250      uf250-shaped random 3-SAT (n=250, m=1065): the searches that
+               finish (all of them SAT) -- ~30 min on 8 cores
+    unsat150   random 3-SAT n=150, m=639 (alpha 4.26): mostly UNSAT, searches
+               exhausting both branches of every decision (~40 k nodes)
+    unsat200   random 3-SAT n=200, m=852: UNSAT searches of 10^5-10^6 nodes
+               (~1 min on 6 cores)
+    python tests/golden/make_fullsolve.py [set]      (default: uf250)
 
 The checker is the C oracle (oracle/sat_oracle.c, SOUND mode), itself pinned to
 the reference's dpll_optimized with only its branch statement rewritten
@@ -26,9 +30,13 @@ sys.path.insert(0, ROOT)
 from satmi import cnf  # noqa: E402
 from oracle import oracle  # noqa: E402
 
-N, M, K, SEED, COUNT = 250, 1065, 3, 250, 96
-NODE_CAP = 1_200_000   # most uf250-shaped searches need more: the fixture keeps the ones that finish
-OUT = os.path.join(HERE, "fullsolve_uf250.json")
+# set: (n, m, k, seed, count, node cap) -- the fixture keeps the searches that finish within the cap
+SETS = {"uf250": (250, 1065, 3, 250, 96, 1_200_000),
+        "unsat150": (150, 639, 3, 150, 24, 2_000_000),
+        "unsat200": (200, 852, 3, 200, 12, 2_000_000)}
+SET = sys.argv[1] if len(sys.argv) > 1 else "uf250"
+N, M, K, SEED, COUNT, NODE_CAP = SETS[SET]
+OUT = os.path.join(HERE, f"fullsolve_{SET}.json")
 
 
 def solve(i):
@@ -41,7 +49,7 @@ def main():
     b = cnf.uniform_ksat(COUNT, N, M, K, seed=SEED)
     sha = hashlib.sha256(b.lits.tobytes()).hexdigest()
     cases = []
-    with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+    with ProcessPoolExecutor(max_workers=min(6, os.cpu_count() or 1)) as ex:
         for i, o in ex.map(solve, range(COUNT)):
             print(i, o["status"], o["counters"]["nodes"], flush=True)
             if o["counters"]["nodes"] > NODE_CAP:

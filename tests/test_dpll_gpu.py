@@ -164,20 +164,24 @@ def test_configs4_batch_properties(n, m, k, cap, B):
         assert r.counter_dict(b) == {**r.counter_dict(b), **{k_: o["counters"][k_] for k_ in CTR}}
 
 
+@pytest.mark.parametrize("fixture,min_unsat", [("uf250", 0), ("unsat150", 5), ("unsat200", 5)])
 @pytest.mark.parametrize("split", [_capi.SPLIT_OFF, _capi.SPLIT_ALWAYS])
-def test_configs4_uf250_solved_to_completion(golden_dir, split):
-    """configs[4] uf250-shaped searches run to the end (no node cap; 10^5-10^6
-    calls each): status, every counter and the model equal the oracle's
-    (tests/golden/fullsolve_uf250.json, make_fullsolve.py), with and without
-    branch splitting (24 searches on thousands of idle waves: helpers take
-    subtrees of searches a million calls deep)."""
-    with open(os.path.join(golden_dir, "fullsolve_uf250.json")) as fh:
+def test_configs4_solved_to_completion(golden_dir, fixture, min_unsat, split):
+    """configs[4]-scale searches run to the end (no node cap): uf250-shaped SAT
+    searches of 10^3-10^6 calls, and UNSAT searches at n=150 / n=200 that
+    exhaust both branches of every decision (REF.py:167-214; 10^4-10^6 calls):
+    status, every counter and the model equal the oracle's
+    (tests/golden/fullsolve_<fixture>.json, make_fullsolve.py), with and
+    without branch splitting (a few searches on thousands of idle waves:
+    helpers take subtrees of searches a million calls deep)."""
+    with open(os.path.join(golden_dir, f"fullsolve_{fixture}.json")) as fh:
         g = json.load(fh)
     batch = cnf.uniform_ksat(g["count"], g["n"], g["m"], g["k"], seed=g["seed"])
     import hashlib
     assert hashlib.sha256(batch.lits.tobytes()).hexdigest() == g["lits_sha256"]
     cases = g["cases"]
     assert len(cases) >= 8
+    assert sum(c["status"] == _capi.DPLL_EXHAUSTED for c in cases) >= min_unsat
     fs = [batch.instance(c["index"]) for c in cases]   # only the searches the oracle finished
     _capi.set_split(split)
     try:
@@ -372,6 +376,37 @@ def test_sound_kernels_match_reference_fixture(golden_dir, policy):
         assert got["solutions"] == c["full"]["solutions"]
         first = r.solutions(b)[0] if got["solutions"] else None
         assert first == c["full"]["first_solution"], (policy, c["tag"])
+
+
+@pytest.mark.parametrize("tag", ["configs1_n50", "configs2_n100"])
+@pytest.mark.parametrize("split", [_capi.SPLIT_OFF, _capi.SPLIT_ALWAYS])
+def test_bench_kernel_matches_reference_fixture(golden_dir, tag, split):
+    """The kernel behind the headline (dpll_fixed_kernel: K = 3, n <= 127,
+    m <= 448) directly against the reference's own vectors of the bench
+    shapes (tests/golden/dpll_sound_ref.json, make_golden_sound.py), one K = 3
+    batch per tag so that the launch takes the fixed class; unsplit, and split
+    with every search allowed to donate from its first check (warm-up 0)."""
+    cases = [c for c in _golden(golden_dir, "dpll_sound_ref.json") if c["tag"] == tag]
+    assert len(cases) >= 64
+    fs = [c["formula"] for c in cases]
+    n = max(abs(l) for f in fs for cl in f for l in cl)
+    m = max(len(f) for f in fs)
+    assert all(len(cl) == 3 for f in fs for cl in f)
+    kern, lds, _ = _capi.plan(n, m, 3 * m, 3)
+    assert kern == _capi.KERNEL_INC and lds == 5108, "not dpll_fixed_kernel's shape class"
+    _capi.set_split(split)
+    _capi.set_split_warmup(0)
+    try:
+        r = dpll_batch(fs, mode="sound", max_solutions=1, sol_cap=1)
+    finally:
+        _capi.set_split(True)
+        _capi.set_split_warmup(-1)
+    for b, c in enumerate(cases):
+        got = r.counter_dict(b)
+        for k in ("nodes", "decisions", "unit_props", "pure_assigns", "conflicts"):
+            assert got[k] == c["first"]["counters"][k], (tag, b, k)
+        want = [] if c["first"]["model"] is None else [c["first"]["model"]]
+        assert r.solutions(b) == want, (tag, b)
 
 
 @pytest.mark.parametrize("n,m,cap", [(200, 700, 800), (300, 1100, 500)])

@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 for i in $(seq 1 $REPS); do
   for lib in "$@"; do
-    SATMI_LIB_VARIANT=$lib timeout -k 10 300 python bench.py --no-cpu-baseline $ARGS > $OUT/${lib%.so}_$i.json 2>/dev/null || { echo "bench $lib failed"; exit 1; }
+    SATMI_LIB_VARIANT=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-legs $ARGS > $OUT/${lib%.so}_$i.json 2>/dev/null || { echo "bench $lib failed"; exit 1; }
     python -c "import json; d=json.load(open('$OUT/${lib%.so}_$i.json')); print('$lib', round(d['value']), round(d['roofline']['kernel_ms'],1))"
   done
 done
