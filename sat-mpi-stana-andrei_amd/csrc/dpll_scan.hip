@@ -160,8 +160,9 @@ struct SLds {
     typename Pack<K>::W *cls;   // [mcap rounded up to 64]  packed literal codes per clause
     uint8_t *lv;                // [2(ncap+1)]  literal state bytes
     uint32_t *ts;               // [ncap+1]  snapshot index of the assignment in the running batch
-    uint32_t *cnt;              // [ncap+1]  free occurrences in active clauses, pos | neg << 16
-    uint32_t *first;            // [ncap+1]  first free occurrence, position c << 3 | slot
+    uint32_t *cnt;              // [2(ncap+1)]  free occurrences in active clauses, per literal code
+    uint32_t *first;            // [ncap+1]  flags / first positions of choose()'s scans (the fixed
+                                //           kernel: the ts array, see dpll_fixed_kernel)
     C *trail;                   // [ncap+1]  assignment order (literal codes) == dict insertion order
     C *fvar;                    // [ncap+1]  decision frames: var | PHASE_BIT once False runs
     C *ftrail;                  // [ncap+1]  trail length before the decision
@@ -607,10 +608,12 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
 }
 
 // literal_sign / var_counts scan (REF.py:174-179, :198-203): every free
-// occurrence in an active clause is counted per variable.  Returns whether
-// any clause is active (none: REF.py:170-171).  Within an active clause the
-// atomic runs for every slot -- a falsified slot adds 0, padding hits
-// variable 0 (never read) -- so there is no branch per slot.  The dict order
+// occurrence in an active clause is counted per literal code.  Returns whether
+// any clause is active (none: REF.py:170-171).  In an active clause a slot's
+// state byte is 1 (free) or 0 (false; a true slot would make the clause
+// inactive), which is the slot's count increment as it is: the atomic runs
+// for every slot with no branch and no arithmetic (padding adds 0 to code
+// 0, never read).  The dict order
 // (first positions) is not tracked here: only the branch candidates and the
 // pure literals need it, and choose() finds those afterwards (a per-slot
 // atomicMin of the first position here cost 21 LDS atomics per node, most of
@@ -626,10 +629,9 @@ __device__ int scan_counts(const SLds<K, C> &S, int mpad) {
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const uint32_t code = field<K>(w, j);
-                const bool fr = (x[j] & 1u) != 0u;
-                atomicAdd(&S.cnt[code >> 1], fr ? ((code & 1u) ? 0x10000u : 1u) : 0u);
+                atomicAdd(&S.cnt[code], x[j]);
 #ifdef SATMI_DUP_CNT
-                atomicAdd(&S.cnt[code >> 1], opaque_zero());
+                atomicAdd(&S.cnt[code], opaque_zero());
 #endif
             }
         }
@@ -712,7 +714,7 @@ struct Choice {
 // assignment's dict order).
 template <int K, typename C>
 __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
-    const int ln = lane_id();
+    const int ln = lane_id_here();   // per call: lane-invariant addresses hoisted out of the node loop spill
     const uint64_t lt = lanemask_lt();
     int npure = 0;
     uint32_t lmax = 0;
@@ -721,8 +723,8 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
         const int v = v0 + ln;
         const uint32_t vc = (uint32_t)min(v, n);
         const bool live = (v <= n) & var_free(S.lv, vc);
-        const uint32_t c = S.cnt[vc];
-        const uint32_t p = c & 0xFFFFu, q = c >> 16;
+        const uint2 c = ((const uint2 *)S.cnt)[vc];   // the counts of codes 2v, 2v + 1
+        const uint32_t p = c.x, q = c.y;
         lmax = live ? max(lmax, p + q) : lmax;
         npure += __popcll(__ballot(live & ((p + q) != 0u) & ((p == 0u) | (q == 0u))));
     };
@@ -740,8 +742,8 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
         const int v = v0 + ln;
         const uint32_t vc = (uint32_t)min(v, n);
         const bool live = (v <= n) & var_free(S.lv, vc);
-        const uint32_t c = S.cnt[vc];
-        const uint32_t p = c & 0xFFFFu, q = c >> 16;
+        const uint2 c = ((const uint2 *)S.cnt)[vc];
+        const uint32_t p = c.x, q = c.y;
         const bool pure = live & ((p + q) != 0u) & ((p == 0u) | (q == 0u));
         const bool cand = live & (p + q == maxc);
         const uint64_t cm = __ballot(cand);
@@ -749,7 +751,7 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
         ncand += __popcll(cm);
         const uint32_t vw = v <= n ? vc : 0u;
         S.first[vw] = npure ? (pure ? NONE32 : 0u) : (cand ? 1u : 0u);
-        S.cnt[vw] = 0u;   // cleared for the next scan
+        ((uint2 *)S.cnt)[vw] = make_uint2(0u, 0u);   // cleared for the next scan
     };
     if constexpr (sizeof(C) == 1) {
         if (n >= 1) flag_step(1);
@@ -757,7 +759,7 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
     } else {
         for (int v0 = 1; v0 <= n; v0 += 64) flag_step(v0);
     }
-    S.cnt[0] = 0u;   // variable 0: the padding slots' counts (never read)
+    ((uint2 *)S.cnt)[0] = make_uint2(0u, 0u);   // variable 0: the padding slots' counts (never read)
     S.first[0] = 0u;
     wave_sync();
     uint32_t best = 0;
@@ -825,7 +827,7 @@ enum { ST_PROPAGATE = 0, ST_ANALYZE = 1, ST_BACKTRACK = 2, ST_DONE = 3 };
 // Incremental kernel: occurrence lists of the staged clauses, S.occ[S.occ_off[x] ..
 // S.occ_off[x+1]) = the clauses holding literal code x (each clause once, in no
 // particular order -- the unit bitmap restores clause order).  cnt is borrowed
-// as the per-variable counter / fill cursor and left zeroed.
+// as the per-code counter / fill cursor and left zeroed.
 template <int K, typename C>
 __device__ void build_occurrences(const SLds<K, C> &S, uint16_t *occ, int m, int n) {
     using W = typename Pack<K>::W;
@@ -844,30 +846,27 @@ __device__ void build_occurrences(const SLds<K, C> &S, uint16_t *occ, int m, int
             }
         }
     };
-    each_slot([&](int, uint32_t code) { atomicAdd(&S.cnt[code >> 1], (code & 1u) ? 0x10000u : 1u); });
+    each_slot([&](int, uint32_t code) { atomicAdd(&S.cnt[code], 1u); });
     wave_sync();
     int carry = 0;
-    for (int v0 = 0; v0 <= n; v0 += 64) {
-        const int v = v0 + ln;
-        const uint32_t cv = v <= n ? S.cnt[v] : 0u;
-        const int p = (int)(cv & 0xFFFFu), q = (int)(cv >> 16);
-        const int in = wave_incl_scan(p + q);
-        if (v <= n) {
-            const int ex = carry + in - (p + q);
-            S.occ_off[2 * v] = (uint16_t)ex;
-            S.occ_off[2 * v + 1] = (uint16_t)(ex + p);
-            S.cnt[v] = 0u;
+    for (int x0 = 0; x0 < 2 * (n + 1); x0 += 64) {
+        const int x = x0 + ln;
+        const int cx = x < 2 * (n + 1) ? (int)S.cnt[x] : 0;
+        const int in = wave_incl_scan(cx);
+        if (x < 2 * (n + 1)) {
+            S.occ_off[x] = (uint16_t)(carry + in - cx);
+            S.cnt[x] = 0u;
         }
         carry += lane63(in);
     }
     if (ln == 0) S.occ_off[2 * (n + 1)] = (uint16_t)carry;
     wave_sync();
     each_slot([&](int c, uint32_t code) {
-        const uint32_t old = atomicAdd(&S.cnt[code >> 1], (code & 1u) ? 0x10000u : 1u);
-        occ[S.occ_off[code] + ((old >> ((code & 1u) << 4)) & 0xFFFFu)] = (uint16_t)c;
+        const uint32_t old = atomicAdd(&S.cnt[code], 1u);
+        occ[S.occ_off[code] + old] = (uint16_t)c;
     });
     wave_sync();
-    for (int v = ln; v <= n; v += 64) S.cnt[v] = 0u;
+    for (int x = ln; x < 2 * (n + 1); x += 64) S.cnt[x] = 0u;
     // the lists are read back by this wave only: complete the stores first
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     wave_sync();
@@ -1182,9 +1181,8 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
             } else {
                 lv_clear(S.lv, (uint32_t)v);
             }
-            S.ts[v] = 0u;
-            S.cnt[v] = 0u;
-            S.first[v] = NONE32;
+            S.ts[v] = 0u;   // (the fixed kernel's `first` flags alias ts: set by choose() before use)
+            ((uint2 *)S.cnt)[v] = make_uint2(0u, 0u);
         }
     }
     if (__ballot(bad)) {
@@ -1593,7 +1591,10 @@ __global__ void __launch_bounds__(64, SATMI_SCAN_WAVES_PER_SIMD) dpll_fixed_kern
     static_assert(FIXM % 64 == 0, "whole 64-clause chunks");
     __shared__ __attribute__((aligned(16))) uint32_t cls_s[FIXM];
     __shared__ __attribute__((aligned(16))) uint8_t lv_s[2 * (FIX_NCAP + 1)];
-    __shared__ __attribute__((aligned(16))) uint32_t ts_s[FIX_NCAP + 1], cnt_s[FIX_NCAP + 1], first_s[FIX_NCAP + 1];
+    // cnt: one word per literal code; choose()'s `first` flags live in ts (a
+    // flag is < 0x10000 here -- m <= FIXM positions -- so it never matches a
+    // stamp of an epoch >= 1, nor outranks one in atomicMax)
+    __shared__ __attribute__((aligned(16))) uint32_t ts_s[FIX_NCAP + 1], cnt_s[2 * (FIX_NCAP + 1)];
     __shared__ __attribute__((aligned(16))) uint8_t trail_s[FIX_NCAP + 1], fvar_s[FIX_NCAP + 1],
         ftrail_s[FIX_NCAP + 1];
     // snapshot (<= FIXM + 1 byte codes) / pure-literal positions (<= 128 words)
@@ -1606,7 +1607,7 @@ __global__ void __launch_bounds__(64, SATMI_SCAN_WAVES_PER_SIMD) dpll_fixed_kern
     S.lv = lv_s;
     S.ts = ts_s;
     S.cnt = cnt_s;
-    S.first = first_s;
+    S.first = ts_s;
     S.trail = trail_s;
     S.fvar = fvar_s;
     S.ftrail = ftrail_s;
@@ -1652,7 +1653,7 @@ bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, bool inc, u
     lay->lv = o;      o = align16(o + (with_lv ? 2 * N : 0u));   // one-wave kernel: static LDS instead
     lay->cls = o;     o = align16(o + (K == 3 ? 4u : 8u) * Mpad);
     lay->ts = o;      o = align16(o + 4 * N);
-    lay->cnt = o;     o = align16(o + 4 * N);
+    lay->cnt = o;     o = align16(o + 8 * N);
     lay->first = o;   o = align16(o + 4 * N);
     lay->trail = o;   o = align16(o + cb * N);
     lay->fvar = o;    o = align16(o + cb * N);

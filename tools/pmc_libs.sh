@@ -14,7 +14,7 @@ for lib in "$@"; do
   SATMI_LIB_VARIANT=$lib timeout -s KILL 150 rocprofv3 --pmc $CTRS --output-format csv -d "$ROOT/$OUT/$name" -o pmc \
       -- python bench.py --steps 1 --warmup 0 --profile-steps $ARGS > "$OUT/$name.json" 2> "$OUT/$name.err"
   echo "== $lib" >> "$OUT/summary.txt"
-  python tools/pmc_sum.py "$(find "$OUT/$name" -name '*counter_collection.csv' | head -1)" >> "$OUT/summary.txt"
+  python tools/pmc_sum.py "$(find "$OUT/$name" -name "*counter_collection.csv" | head -1)" >> "$OUT/summary.txt" && rm -rf "$OUT/$name"
   echo "$lib ok"
 done
 cat "$OUT/summary.txt"
