@@ -99,6 +99,7 @@ __device__ __forceinline__ uint32_t opaque_zero() {
 constexpr uint32_t LV_TRUE = 8u, LV_FALSE = 0u, LV_FREE = 1u;
 constexpr uint32_t CODE_PAD = 0u, CODE_DUMMY = 1u;
 __device__ __forceinline__ bool sum_true(uint32_t s) { return (s & 0xF8u) != 0u; }
+__device__ __forceinline__ bool sum_open(uint32_t s) { return s < 8u; }
 __device__ __forceinline__ uint32_t sum_nfree(uint32_t s) { return s & 7u; }
 
 template <int K>
@@ -177,7 +178,9 @@ struct SLds {
 
 // literal `code` becomes true: one 2-byte store sets both literals of its variable
 __device__ __forceinline__ void lv_assign(uint8_t *lv, uint32_t code) {
-    *(uint16_t *)(lv + (code & ~1u)) = (uint16_t)((code & 1u) ? (LV_TRUE << 8) : LV_TRUE);
+    // two byte stores (LDS issue) instead of one 16-bit store of a selected value (VALU issue)
+    lv[code] = (uint8_t)LV_TRUE;
+    lv[code ^ 1u] = (uint8_t)LV_FALSE;
 }
 __device__ __forceinline__ void lv_clear(uint8_t *lv, uint32_t v) {
     *(uint16_t *)(lv + 2 * v) = (uint16_t)(LV_FREE | (LV_FREE << 8));
@@ -256,14 +259,21 @@ __device__ __forceinline__ uint32_t clause_sum(const uint32_t (&x)[K]) {
     return s;
 }
 
-// The literal of a unit clause: its one free slot.
+// The literal of a unit clause: its one free slot.  (A unit clause has no
+// true slot, so each state byte is 0 or 1: for K = 3 the free slot's field
+// offset is 10 x[1] + 20 x[2], one extract.)
 template <int K>
 __device__ __forceinline__ uint32_t unit_code(typename Pack<K>::W w, const uint32_t (&x)[K]) {
-    uint32_t code = field<K>(w, 0);
+    if constexpr (K == 3) {
+        return __builtin_amdgcn_ubfe((uint32_t)w, x[1] * (uint32_t)Pack<3>::BITS + x[2] * (2u * Pack<3>::BITS),
+                                     Pack<3>::BITS);
+    } else {
+        uint32_t code = field<K>(w, 0);
 #pragma unroll
-    for (int j = 1; j < K; ++j)
-        if (x[j] & 1u) code = field<K>(w, j);
-    return code;
+        for (int j = 1; j < K; ++j)
+            if (x[j] & 1u) code = field<K>(w, j);
+        return code;
+    }
 }
 
 // Snapshot stamps ts[v]: epoch << 16 | (0xFFFF - k) for the variable of
@@ -271,7 +281,7 @@ __device__ __forceinline__ uint32_t unit_code(typename Pack<K>::W w, const uint3
 // clearing: an older epoch is smaller, and atomicMax keeps the first entry of
 // a variable (the smallest k) within the current one.
 constexpr uint32_t EPOCH_LIMIT = 0xFFFFu - 4096u;   // > rounds of one propagate call (<= n+1 <= 2048)
-__device__ __forceinline__ uint32_t stamp(uint32_t ep, uint32_t k) { return (ep << 16) | (0xFFFFu - k); }
+__device__ __forceinline__ uint32_t stamp(uint32_t ep, uint32_t k) { return ((ep << 16) | 0xFFFFu) - k; }   // k <= 0xFFFF
 __device__ __forceinline__ uint32_t stamp_index(uint32_t st) { return 0xFFFFu - (st & 0xFFFFu); }
 
 // Scan for unit_propagate: the unit-clause snapshot (REF.py:143), in clause
@@ -373,15 +383,13 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 d = ln >= eb ? db : d;
             }
             const bool valid = ln < total;
-            const uint32_t c = S.occ[valid ? d + ln : 0];
+            const uint32_t c = S.occ[(uint32_t)(valid ? d + ln : 0)];   // 32-bit offset from the wave's base
             const W w = cls_at(S, c);
             uint32_t x[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) x[j] = lv_get(S, field<K>(w, j));
-            const uint32_t s = clause_sum<K>(x);
-            const bool open = valid && !sum_true(s);
-            const uint32_t nf = sum_nfree(s);
-            const bool empty = open && nf == 0u;
+            const uint32_t sv = valid ? clause_sum<K>(x) : 0xFFu;
+            const bool empty = sv == 0u;
             if (__builtin_expect(__ballot(empty) != 0ull, 0)) {
                 const int et = emptier<K>(S, w, bep);   // every lane: no exec-mask branch
                 const int e = empty ? et : INT_MAX;
@@ -389,7 +397,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 return 0;
             }
             *empty_at = INT_MAX;
-            const bool unit = open && nf == 1u;
+            const bool unit = sv == 1u;
             const uint64_t um = __ballot(unit);
             const int nun = __popcll(um);
             if (__builtin_expect(nun <= FAST_UNITS, 1)) {
@@ -555,11 +563,13 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             const bool valid = k < nu;
             const uint32_t code = (uint32_t)S.snap[valid ? k : 0];   // predicated loads
             const uint32_t v = code >> 1;
+            // lanes past nu read entry 0, whose variable is stamped with index 0
+            // != k: never first.  (One compare: its ballot folds into the v_cmp.)
 #ifdef SATMI_DUP_ASSIGN
-            const bool first = valid & (S.ts[v] == stamp(bep, (uint32_t)k)) &
-                               ((((const volatile uint32_t *)S.ts)[v] & opaque_zero()) == 0u);
+            const bool first = (S.ts[v] | (((const volatile uint32_t *)S.ts)[v] & opaque_zero())) ==
+                               stamp(bep, (uint32_t)k);
 #else
-            const bool first = valid & (S.ts[v] == stamp(bep, (uint32_t)k));
+            const bool first = S.ts[v] == stamp(bep, (uint32_t)k);
 #endif
             const uint64_t mk = __ballot(first);
             // predicated stores (no exec-mask branch): the other lanes write
@@ -623,7 +633,7 @@ __device__ int scan_counts(const SLds<K, C> &S, int mpad) {
     using W = typename Pack<K>::W;
     uint64_t any = 0;   // only "no active clause" matters: OR the ballots (one scalar op per chunk)
     for_chunks<K, Pack<K>::UNROLL>(S, mpad, [&](int, W w, const uint32_t(&x)[K]) {
-        const bool act = !sum_true(clause_sum<K>(x));
+        const bool act = sum_open(clause_sum<K>(x));
         any |= __ballot(act);
         if (act) {
 #pragma unroll
