@@ -32,7 +32,7 @@ child process after the headline -- the line's `configs` object):
     php-res    configs[3]: resolution saturation of PHP(4,3) (pair kernel +
                hash dedup), its first 4 passes (171,392 derived clauses; the
                5th pass would resolve 1.5e10 pairs) -- derived clauses/s
-    cdcl       the reference's CDCLSolver (REF.py:217-384) on 4,096 menu-sized
+    cdcl       the reference's CDCLSolver (REF.py:217-384) on 32,768 menu-sized
                formulas (generate_large_formula(80, 3, 15), REF.py:21-29, the
                shape of rezultat.txt:178-188), <= 10,000 iterations each --
                formulas/s
@@ -74,13 +74,14 @@ WORKLOADS = {
 # configs[3] presets: (holes, resolution passes) -- one formula per step, host-array C ABI
 SATURATION = {"php-dp": (5, 0), "php-res": (3, 4)}
 # CDCL preset: (formulas per step, clauses, max literals per clause, variables, max_iter, seed)
-CDCL = {"cdcl": (4096, 80, 3, 15, 10000, 1234)}
+CDCL = {"cdcl": (32768, 80, 3, 15, 10000, 1234)}
 
 # the secondary legs of the default N = 1 line: (name, workload, extra args)
 LEGS = [
     ("configs[1] 2 streams", "3sat-n50", ["--streams", "2", "--steps", "32", "--warmup", "4"]),
     ("configs[1] 16 streams", "3sat-n50", ["--streams", "16", "--steps", "128", "--warmup", "16"]),
     ("configs[3] php-dp", "php-dp", ["--steps", "40", "--warmup", "3"]),
+    ("configs[3] php-dp 8 threads", "php-dp", ["--steps", "10", "--warmup", "2", "--threads", "8"]),
     ("configs[3] php-res", "php-res", ["--steps", "20", "--warmup", "2"]),
     ("configs[4] uf250", "uf250", ["--steps", "4", "--warmup", "1"]),
     ("configs[4] 5sat-n200", "5sat-n200", ["--steps", "4", "--warmup", "1"]),
@@ -115,6 +116,8 @@ def parse(argv=None):
     p.add_argument("--split-warmup", type=int, default=-1,
                    help="nodes before a search may donate (satmi_dpll_set_split_warmup; -1 = default)")
     p.add_argument("--helpers-per-cu", type=int, default=0, help="branch-splitting helpers per CU (0 = library default)")
+    p.add_argument("--threads", type=int, default=1,
+                   help="php-dp: concurrent solves per step, one host thread (and HIP stream) each")
     p.add_argument("--streams", type=int, default=None, choices=range(1, 17),
                    help="HIP streams (each with its own resident batch) the steps rotate over (default: 16 for "
                         "3sat-n50, whose 4,096 short searches leave most CU slots idle for a launch's 2 ms, else 2)")
@@ -554,17 +557,27 @@ def run_saturation(args, world, rank, local):
     from satmi.dp import last_stats as dp_stats
     from satmi.resolution import last_stats as res_stats
     from satmi.resolution import resolve
+    from concurrent.futures import ThreadPoolExecutor
     torch.cuda.set_device(local)
     holes, npass = SATURATION[args.workload]
     f = cnf.pigeonhole(holes)
+    T = max(1, args.threads) if args.workload == "php-dp" else 1
     if args.workload == "php-dp":
-        run = lambda: eliminate(f)                                  # noqa: E731
+        def one():   # statistics are per host thread: read them in the thread that solved
+            torch.cuda.set_device(local)
+            r = eliminate(f)
+            return r, dp_stats()
         work = lambda r: 1                                          # noqa: E731
         unit, metric_desc = "solves/s", f"Davis-Putnam elimination of PHP({holes + 1},{holes})"
     else:
-        run = lambda: resolve(f, max_passes=npass)                  # noqa: E731
+        def one():
+            r = resolve(f, max_passes=npass)
+            return r, res_stats()
         work = lambda r: sum(r["pass_new"])                         # noqa: E731
         unit, metric_desc = "derived clauses/s", f"resolution saturation of PHP({holes + 1},{holes}), first {npass} passes"
+    pool = ThreadPoolExecutor(T) if T > 1 else None
+    # a step: T concurrent solves (one host thread and HIP stream each; T = 1: one solve)
+    run = (lambda: list(pool.map(lambda _: one(), range(T)))) if pool else (lambda: [one()])   # noqa: E731
     for _ in range(0 if args.profile_steps else args.warmup):
         run()
     torch.cuda.synchronize()
@@ -575,9 +588,11 @@ def run_saturation(args, world, rank, local):
     last = None
     stats = []
     for _ in range(args.steps):
-        last = run()
-        done += work(last)
-        stats.append(res_stats() if args.workload == "php-res" else dp_stats())
+        outs = run()
+        for r, st in outs:
+            done += work(r)
+            stats.append(st)
+        last = outs[-1][0]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -586,11 +601,15 @@ def run_saturation(args, world, rank, local):
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    if pool:
+        pool.shutdown()
     out = {"metric": METRIC, "value": done * world / elapsed, "unit": unit, "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic: pigeonhole formula",
-           "config": {"workload": metric_desc + " (BASELINE configs[3]); replicas across ranks",
-                      "preset": args.workload, "parallelism": f"replicas x{world}"},
+           "config": {"workload": metric_desc + " (BASELINE configs[3]); replicas across ranks"
+                                  + (f"; {T} concurrent solves per step (host threads, one HIP stream each)" if T > 1
+                                     else ""),
+                      "preset": args.workload, "parallelism": f"replicas x{world}", "concurrent_solves": T},
            "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
            "roofline": saturation_roofline(stats) if args.workload == "php-res" else
            dp_roofline(stats, torch.cuda.get_device_properties(local).multi_processor_count, SHADER_CLOCK_HZ)}
@@ -621,15 +640,10 @@ def run_cdcl(args, world, rank, local):
     call over the preset's formulas (host arrays in, verdicts out), each run to
     its verdict or max_iter iterations (the reference's own loop is unbounded;
     its driver times it out).  Replicas across ranks."""
-    import random
-
-    from satmi import solvers
     from satmi.cdcl import CDCL_LIMIT, CDCL_SAT, CDCL_UNSAT, cdcl_batch_packed
     torch.cuda.set_device(local)
     nf, ncl, maxlit, nvar, max_iter, seed = CDCL[args.workload]
-    random.seed(seed)
-    formulas = [solvers.generate_large_formula(ncl, maxlit, nvar) for _ in range(nf)]
-    hb = cnf.pack(formulas)   # the CSR host arrays the C ABI takes, packed once
+    hb = cnf.menu_batch(nf, ncl, maxlit, nvar, seed=seed)   # the CSR host arrays the C ABI takes
     for _ in range(0 if args.profile_steps else args.warmup):
         cdcl_batch_packed(hb, max_iter=max_iter)
     if world > 1:
@@ -651,8 +665,8 @@ def run_cdcl(args, world, rank, local):
     out = {"metric": METRIC, "value": nf * args.steps * world / elapsed, "unit": "formulas/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32/f64 activities",
-           "data": f"synthetic: {nf} x generate_large_formula({ncl}, {maxlit}, {nvar}) (REF.py:21-29, "
-                   f"random.seed({seed}))",
+           "data": f"synthetic: {nf} formulas of generate_large_formula({ncl}, {maxlit}, {nvar})'s distribution "
+                   f"(REF.py:21-29; satmi.cnf.menu_batch, seed {seed})",
            "config": {"workload": f"cdcl_solve (REF.py:382-384) on {nf} formulas, <= {max_iter} iterations each; "
                                   f"replicas across ranks", "preset": args.workload,
                       "parallelism": f"replicas x{world}"},
@@ -664,7 +678,7 @@ def run_cdcl(args, world, rank, local):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         for i in range(0, nf, max(1, nf // 16)):   # verdicts checked against the oracle on a sample
-            o = oracle.cdcl(formulas[i], max_iter=max_iter)
+            o = oracle.cdcl(hb.instance(i), max_iter=max_iter)
             g = {CDCL_SAT: 1, CDCL_UNSAT: 0, CDCL_LIMIT: -1}.get(res[i]["status"], -2)
             if o["result"] != g or (g == 1 and o["assignment"] != res[i]["assignment"]):
                 raise SystemExit(f"bench: GPU and oracle disagree on CDCL formula {i}")

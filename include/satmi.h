@@ -152,13 +152,15 @@ int satmi_resolution_debug_slot_base(int64_t base);
  *   s is rec_step_off[s-1] .. rec_step_off[s] in rec_clause_off / rec_lits,
  *   every clause in its Python set iteration order; rec_step_off[s] is left
  *   untouched for a step that ended the elimination.
+ * Thread-safe: each host thread runs its calls on its own HIP stream and
+ * device buffers (kept between calls), so solves from several threads overlap.
  */
 int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_lits, int64_t step_limit,
                   int64_t clause_limit, double time_limit_s, int32_t *h_result, int32_t *h_trace_vars,
                   int trace_cap, int32_t *h_steps, int32_t *h_rec_lits, int64_t rec_lit_cap,
                   int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_step_off, int rec_step_cap);
 
-/* Work of the last satmi_dp_host call's subsumption filter (REF.py:122-125):
+/* Work of the calling thread's last satmi_dp_host call's subsumption filter (REF.py:122-125):
  * elimination steps, subset tests performed, new (non-tautological) clauses
  * filtered, bytes of candidate keys, key words per clause, and the filter's
  * device time (HIP events on its stream), for rooflines. */

@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -655,6 +656,20 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     return max_vars >= 0 && max_vars < (1 << 29);
 }
 
+// Device memory of satmi_cdcl_batch_host, kept between calls (grow-only, per
+// device): the per-wave arenas of a batch are sized for max_iter learned
+// clauses and reach gigabytes, whose hipMalloc / hipFree per call cost more
+// than the solves of a menu-sized batch.  Calls are serialised on it (each
+// call drains its stream before returning).
+struct CdclScratch {
+    std::mutex mu;
+    std::vector<std::pair<void *, size_t>> dev;   // per device: pointer, bytes
+};
+CdclScratch &cdcl_scratch() {
+    static CdclScratch *c = new CdclScratch;   // never destroyed: no hipFree after the runtime's teardown
+    return *c;
+}
+
 }  // namespace
 }  // namespace satmi
 
@@ -730,8 +745,18 @@ extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_cl
     const size_t o_wc = o_vi + up(8 * (size_t)num_instances);
     const size_t o_arena = o_wc + 256;
     const size_t total = o_arena + (size_t)grid * (size_t)lay.bytes;
-    unsigned char *d = nullptr;
-    SATMI_HIP(hipMalloc(&d, total));
+    CdclScratch &cs = cdcl_scratch();
+    std::lock_guard<std::mutex> lk(cs.mu);
+    if ((int)cs.dev.size() <= dev) cs.dev.resize(dev + 1, {nullptr, 0});
+    auto &slot = cs.dev[dev];
+    if (slot.second < total) {
+        if (slot.first) (void)hipFree(slot.first);
+        slot = {nullptr, 0};
+        void *p = nullptr;
+        SATMI_HIP(hipMalloc(&p, total));
+        slot = {p, total};
+    }
+    unsigned char *d = (unsigned char *)slot.first;
     hipStream_t s = nullptr;
     int rc = SATMI_OK;
     do {
@@ -775,6 +800,5 @@ extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_cl
         if (e == hipSuccess) e = hipMemcpy(h_var_inc, d + o_vi, 8 * (size_t)num_instances, hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = hip_fail(e, "satmi_cdcl_batch_host: launch / copy back");
     } while (0);
-    (void)hipFree(d);
     return rc;
 }

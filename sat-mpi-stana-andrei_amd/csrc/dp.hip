@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -459,7 +460,37 @@ struct DpStats {
     double subsume_ms = 0.0;
     int words = 0;
 };
-DpStats g_dp_stats;
+thread_local DpStats g_dp_stats;   // the calling thread's last call
+
+// Everything one satmi_dp_host call allocates, kept between calls (grow-only)
+// per host thread and device, with the thread's own non-blocking stream: a
+// solve of a small formula is dozens of steps of small launches with a few
+// host read-backs each, so allocating its ~40 buffers per call cost more than
+// its kernels, and solves from several host threads overlap on the device
+// (each fills a fraction of it).  Never destroyed: no hipFree after the
+// runtime's teardown.
+struct DpWork {
+    Buf d_off, d_lits, d_v2d, d_d2v, misc, firstpos, order, popscratch, base, usedtmp;
+    Buf fpos, fneg, frem, plist, nlist, rlist, scanpos, tiles, grand, counts3, rbits, nontaut, ntlist, kept, klist, kpos,
+        sizes, offs;
+    Gen g[2];
+    Img A, B, R;
+    std::vector<hipEvent_t> ev;   // subsumption-filter timing: one pair per step, read once per call
+    hipStream_t stream = nullptr;
+};
+DpWork *dp_work(int dev) {
+    thread_local std::vector<DpWork *> mine;
+    if ((int)mine.size() <= dev) mine.resize(dev + 1, nullptr);
+    if (!mine[dev]) {
+        DpWork *w = new DpWork;
+        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete w;
+            return nullptr;
+        }
+        mine[dev] = w;
+    }
+    return mine[dev];
+}
 
 // ordered compaction of flag[n] into out (indices); returns the count
 // compact() without the count read-back: `out` is sized for all n, the count
@@ -534,13 +565,24 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     const int V = (int)dense2var.size();
     const int W = std::max(1, (V + 63) / 64);
     const int K = 2 * W;
-    hipStream_t s = nullptr;
-
-    Buf d_off, d_lits, d_v2d, d_d2v, flags, misc, firstpos, order, popscratch, base, usedtmp;
-    Buf fpos, fneg, frem, plist, nlist, rlist, scanpos, tiles, grand, counts3, rbits, nontaut, ntlist, kept, klist, kpos,
-        sizes, offs;
-    Gen g[2];
-    Img A, B, R;
+    int dev_id = 0;
+    SATMI_HIP(hipGetDevice(&dev_id));
+    DpWork *wk = dp_work(dev_id);
+    if (!wk) {
+        set_error("satmi_dp_host: hipStreamCreate failed");
+        return SATMI_ERR_HIP;
+    }
+    DpWork &Wk = *wk;
+    hipStream_t s = Wk.stream;
+    Buf &d_off = Wk.d_off, &d_lits = Wk.d_lits, &d_v2d = Wk.d_v2d, &d_d2v = Wk.d_d2v, &misc = Wk.misc,
+        &firstpos = Wk.firstpos, &order = Wk.order, &popscratch = Wk.popscratch, &base = Wk.base,
+        &usedtmp = Wk.usedtmp;
+    Buf &fpos = Wk.fpos, &fneg = Wk.fneg, &frem = Wk.frem, &plist = Wk.plist, &nlist = Wk.nlist, &rlist = Wk.rlist,
+        &scanpos = Wk.scanpos, &tiles = Wk.tiles, &grand = Wk.grand, &counts3 = Wk.counts3, &rbits = Wk.rbits,
+        &nontaut = Wk.nontaut, &ntlist = Wk.ntlist, &kept = Wk.kept, &klist = Wk.klist, &kpos = Wk.kpos,
+        &sizes = Wk.sizes, &offs = Wk.offs;
+    Gen *g = Wk.g;
+    Img &A = Wk.A, &B = Wk.B, &R = Wk.R;
     DP_TRY(d_off.need(4 * (size_t)(nclauses + 1)));
     DP_TRY(d_lits.need(4 * (size_t)std::max<int64_t>(Ltot, 1)));
     DP_TRY(d_v2d.need(4 * (size_t)(maxvar + 1)));
@@ -565,17 +607,18 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             SATMI_HIP(hipGetLastError());
         }
     }
-    // subsumption-filter timing (satmi_dp_last_stats); misc[40..48) counts its subset tests
-    struct Ev {
-        hipEvent_t e[2] = {nullptr, nullptr};
-        ~Ev() {
-            for (auto x : e)
-                if (x) (void)hipEventDestroy(x);
+    // subsumption-filter timing (satmi_dp_last_stats): an event pair per step,
+    // read after the loop (no per-step wait); misc[40..48) counts its subset tests
+    size_t nev = 0;   // event pairs recorded this call
+    const auto next_events = [&]() -> hipEvent_t * {
+        if (2 * nev + 2 > Wk.ev.size()) {
+            hipEvent_t a = nullptr, b = nullptr;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return nullptr;
+            Wk.ev.push_back(a);
+            Wk.ev.push_back(b);
         }
-    } evs;
-    SATMI_HIP(hipEventCreate(&evs.e[0]));
-    SATMI_HIP(hipEventCreate(&evs.e[1]));
-    hipEvent_t *ev_sub = evs.e;
+        return &Wk.ev[2 * nev++];
+    };
     g_dp_stats = DpStats{};
     g_dp_stats.words = K;
     DP_TRY(firstpos.need(8 * (size_t)std::max(V, 1)));
@@ -686,6 +729,11 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             const uint64_t *rb = rbits.as<uint64_t>();
             int64_t *kp = kept.as<int64_t>();
             unsigned long long *tc = (unsigned long long *)(misc.as<char>() + 40);
+            hipEvent_t *ev_sub = next_events();
+            if (!ev_sub) {
+                set_error("satmi_dp_host: hipEventCreate failed");
+                return SATMI_ERR_HIP;
+            }
             SATMI_HIP(hipEventRecord(ev_sub[0], s));
             if (K <= 8 && (K & 1) == 0) {
                 auto tiled = [&](const int64_t *sel, int64_t nsel, int64_t lo, int64_t hi) {
@@ -719,9 +767,6 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             }
             SATMI_HIP(hipEventRecord(ev_sub[1], s));
             SATMI_HIP(hipGetLastError());
-            SATMI_HIP(hipEventSynchronize(ev_sub[1]));
-            float ms = 0.0f;
-            if (hipEventElapsedTime(&ms, ev_sub[0], ev_sub[1]) == hipSuccess) g_dp_stats.subsume_ms += ms;
             g_dp_stats.new_clauses += m;
             g_dp_stats.candidates_bytes += (nr + m) * K * 8;
             DP_TRY(compact(kept.as<int64_t>(), m, kpos, tiles, grand, klist, &nkept, s));
@@ -804,9 +849,14 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     }
     {
         unsigned long long tests = 0;
-        SATMI_HIP(hipMemcpy(&tests, misc.as<char>() + 40, 8, hipMemcpyDeviceToHost));
+        SATMI_HIP(hipMemcpyAsync(&tests, misc.as<char>() + 40, 8, hipMemcpyDeviceToHost, s));
+        SATMI_HIP(hipStreamSynchronize(s));
         g_dp_stats.tests = (int64_t)tests;
         g_dp_stats.steps = steps;
+        for (size_t i = 0; i < nev; ++i) {   // the stream has drained
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, Wk.ev[2 * i], Wk.ev[2 * i + 1]) == hipSuccess) g_dp_stats.subsume_ms += ms;
+        }
     }
     *h_result = result;
     *h_steps = steps;

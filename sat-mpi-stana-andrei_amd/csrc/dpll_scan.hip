@@ -673,7 +673,7 @@ __device__ uint32_t first_flagged(const SLds<K, C> &S, int mpad) {
         uint32_t pos = NONE32;
 #pragma unroll
         for (int j = K - 1; j >= 0; --j)
-            pos = act & ((x[j] & 1u) != 0u) & (f[j] != 0u) ? (((uint32_t)c << 3) | (uint32_t)j) : pos;
+            pos = (act & ((x[j] & 1u) != 0u) & (f[j] != 0u)) ? (((uint32_t)c << 3) | (uint32_t)j) : pos;
         const uint64_t hit = __ballot(pos != NONE32);
         if (hit) return (uint32_t)__builtin_amdgcn_readlane((int)pos, __builtin_ctzll(hit));
     }

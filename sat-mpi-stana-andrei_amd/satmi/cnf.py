@@ -41,23 +41,23 @@ class CnfBatch:
 
 def pack(formulas):
     """List of formulas (List[List[int]]) -> CnfBatch."""
-    icb = [0]
-    clb = [0]
-    lits = []
-    nv = []
-    for f in formulas:
-        m = 0
-        for clause in f:
-            for lit in clause:
-                if lit == 0:
-                    raise ValueError("literal 0 is not allowed (REF.py:51)")
-                lits.append(int(lit))
-            clb.append(len(lits))
-            m = max([m] + [abs(int(l)) for l in clause])
-        icb.append(len(clb) - 1)
-        nv.append(m)
-    return CnfBatch(np.asarray(icb, dtype=np.int32), np.asarray(clb, dtype=np.int32),
-                    np.asarray(lits if lits else [0], dtype=np.int32), np.asarray(nv, dtype=np.int32))
+    from itertools import chain
+    ncl = np.fromiter((len(f) for f in formulas), dtype=np.int64, count=len(formulas))
+    clen = np.fromiter((len(c) for f in formulas for c in f), dtype=np.int64, count=int(ncl.sum()))
+    lits = np.fromiter(chain.from_iterable(chain.from_iterable(formulas)), dtype=np.int64, count=int(clen.sum()))
+    if lits.size and not lits.all():
+        raise ValueError("literal 0 is not allowed (REF.py:51)")
+    icb = np.concatenate([[0], np.cumsum(ncl)])
+    clb = np.concatenate([[0], np.cumsum(clen)])
+    # largest variable per formula: the max |literal| over its literal range
+    nv = np.zeros(len(formulas), dtype=np.int64)
+    if lits.size:
+        a = np.abs(lits)
+        lo, hi = clb[icb[:-1]], clb[icb[1:]]
+        has = hi > lo
+        nv[has] = np.maximum.reduceat(a, lo[has])
+    return CnfBatch(icb.astype(np.int32), clb.astype(np.int32),
+                    (lits if lits.size else np.zeros(1, np.int64)).astype(np.int32), nv.astype(np.int32))
 
 
 def uniform_ksat(num_instances, n, m, k, seed=0, dtype=np.int32):
@@ -83,6 +83,26 @@ def uniform_ksat(num_instances, n, m, k, seed=0, dtype=np.int32):
     if clb[-1] >= 2 ** 31:
         raise ValueError("batch too large for int32 offsets; split it")
     return CnfBatch(icb, clb.astype(np.int32), lits.astype(np.int32), np.full(B, n, dtype=np.int32))
+
+
+def menu_batch(count, num_clauses, max_literals_per_clause, num_variables, seed=0):
+    """`count` formulas of generate_large_formula's distribution (REF.py:21-29:
+    clause size uniform in 1..max, distinct variables, each negated w.p. 1/2),
+    drawn with numpy for large batches (not the reference's draw sequence: use
+    solvers.generate_large_formula under a seeded `random` for that)."""
+    rng = np.random.default_rng(seed)
+    C, k, n = count * num_clauses, max_literals_per_clause, num_variables
+    if k > n:
+        raise ValueError("more literals per clause than variables")
+    size = rng.integers(1, k + 1, size=C)
+    vars_ = np.argsort(rng.random((C, n)), axis=1)[:, :k] + 1       # a random k-subset, in random order
+    lit = np.where(rng.random((C, k)) < 0.5, -vars_, vars_)
+    lits = lit[np.arange(k)[None, :] < size[:, None]]
+    clb = np.concatenate([[0], np.cumsum(size)])
+    icb = np.arange(count + 1, dtype=np.int64) * num_clauses
+    a = np.abs(lits)
+    nv = np.maximum.reduceat(a, clb[icb[:-1]]) if count and num_clauses else np.zeros(count, np.int64)
+    return CnfBatch(icb.astype(np.int32), clb.astype(np.int32), lits.astype(np.int32), nv.astype(np.int32))
 
 
 def concat(batches):

@@ -74,3 +74,31 @@ def test_limits():
     o = oracle.dp(f, clause_limit=70)
     r = eliminate(f, clause_limit=70)
     assert (r["result"], r["vars"]) == (o["result"], o["vars"])
+
+
+def test_php65_every_step_matches_oracle():
+    """The configs[3] bench formula PHP(6,5) (bench.py --workload php-dp): the
+    30 eliminated variables and all 29 intermediate clause lists (26,693
+    clauses, each in its set iteration order) equal the oracle's, and the
+    verdict is False (REF.py:117-118)."""
+    f = cnf.pigeonhole(5)
+    o = oracle.dp(f, record=True, rec_cap=1 << 22)
+    r = eliminate(f, record=True)
+    assert r["result"] == o["result"] == 0
+    assert r["vars"] == o["vars"] and len(r["vars"]) == 30
+    assert r["clauses"] == o["clauses"][:_completed(o)]
+
+
+def test_concurrent_solves_from_threads():
+    """satmi_dp_host from several host threads at once (each on its own stream
+    and buffers, as bench.py --threads runs it): every solve equals the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    fs = [cnf.pigeonhole(4), cnf.pigeonhole(3)] + [cnf.uniform_ksat(1, 12, 50, 3, seed=s).instance(0)
+                                                   for s in range(6)]
+    want = [oracle.dp(f, record=True) for f in fs]
+    with ThreadPoolExecutor(4) as ex:
+        for _ in range(3):
+            got = list(ex.map(lambda f: eliminate(f, record=True), fs))
+            for f, o, r in zip(fs, want, got):
+                assert (r["result"], r["vars"]) == (o["result"], o["vars"]), f
+                assert r["clauses"] == o["clauses"][:_completed(o)], f

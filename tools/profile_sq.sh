@@ -17,4 +17,5 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_IN
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
     --output-format csv -d "$ROOT/$OUT/sq2" -o sq2 -- python bench.py --total "$B" --steps 1 --warmup 0 --profile-steps "$@" > "$OUT/sq2.json" 2> "$OUT/sq2.err"
 for f in $(find "$OUT/sq1" "$OUT/sq2" -name "*counter_collection.csv"); do python tools/pmc_sum.py "$f"; done > "$OUT/sq_summary.txt"
+rm -rf "$OUT/sq1" "$OUT/sq2"   # per-dispatch rows: only the summary comes back (gpurun_out <= 64 MiB)
 echo done
