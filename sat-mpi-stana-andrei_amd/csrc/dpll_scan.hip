@@ -553,6 +553,9 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
     const uint64_t lt = lanemask_lt();
     int e = INT_MAX;   // set: the round that emptied a clause (handled after the loop)
     int rs = tl;
+    // the decision literal (the first batch's first entry, always assigned or
+    // kept) is not a propagation in REF.py's counters: taken off once here
+    props -= dec ? 1u : 0u;
     while (nu > 0) {
         ++rounds;
         rs = tl;
@@ -594,9 +597,7 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
                                 : scan_units<K>(S, mpad, ++ep, bep, &e);
         ph.mark(PH_UNITS);
         if (__builtin_expect(e != INT_MAX, 0)) break;
-        props += nassign - (dec && nassign > 0 ? 1 : 0);
-        dec = false;
-        if (nassign == 0) break;   // `changed` stayed False (REF.py:141-142)
+        props += nassign;   // >= 1: a snapshot's first entry is always assigned (`changed`, REF.py:141-142)
         nu = nu_next;
     }
     if (e == INT_MAX) return false;
@@ -612,7 +613,7 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
     for (int i = cut + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
     wave_sync();
     tl = cut;
-    props += keep - (dec ? 1 : 0);
+    props += keep;   // >= 1: the batch's first entry (stamp index 0) is kept
     ph.mark(PH_CONFLICT);
     return true;
 }

@@ -315,7 +315,7 @@ struct ResStats {
     int64_t pairs = 0, candidates = 0, keys_tabled = 0;
     double pair_ms = 0.0, claim_ms = 0.0;
 };
-ResStats g_stats;
+thread_local ResStats g_stats;   // the calling thread's last call
 
 // Times launches on one stream: begin() / end() bracket them, total() sums.
 struct EventTimer {
@@ -337,6 +337,7 @@ struct EventTimer {
         return ev[used].first;
     }
     void end(hipStream_t s) { (void)hipEventRecord(ev[used++].second, s); }
+    void reset() { used = 0; }
     double total() {   // after the stream drained
         double ms = 0.0;
         for (size_t i = 0; i < used; ++i) {
@@ -346,6 +347,31 @@ struct EventTimer {
         return ms;
     }
 };
+
+// Device buffers of satmi_resolution_host, kept between calls (grow-only) per
+// host thread and device, with the thread's own non-blocking stream: a
+// saturation of a small formula is a few passes of small launches, so
+// allocating its buffers per call cost more than its kernels, and calls from
+// several threads overlap.  Never destroyed (no hipFree after the runtime's
+// teardown).
+struct ResWork {
+    DevBuf d_off, d_lits, d_map, clauses, cand, counters, table, flag, pos, slotv, tiles, grand;
+    EventTimer t_pairs, t_claims;
+    hipStream_t stream = nullptr;
+};
+ResWork *res_work(int dev) {
+    thread_local std::vector<ResWork *> mine;
+    if ((int)mine.size() <= dev) mine.resize(dev + 1, nullptr);
+    if (!mine[dev]) {
+        ResWork *w = new ResWork;
+        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete w;
+            return nullptr;
+        }
+        mine[dev] = w;
+    }
+    return mine[dev];
+}
 
 }  // namespace
 
@@ -409,9 +435,16 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
     const int W = std::max(1, (V + 63) / 64);
     const int K = 2 * W;
     const int64_t slot_base = g_slot_base;
-    hipStream_t s = nullptr;
-
-    DevBuf d_off, d_lits, d_map, clauses, cand, counters;
+    int dev_id = 0;
+    SATMI_HIP(hipGetDevice(&dev_id));
+    ResWork *wk = res_work(dev_id);
+    if (!wk) {
+        set_error("satmi_resolution_host: hipStreamCreate failed");
+        return SATMI_ERR_HIP;
+    }
+    hipStream_t s = wk->stream;
+    DevBuf &d_off = wk->d_off, &d_lits = wk->d_lits, &d_map = wk->d_map, &clauses = wk->clauses, &cand = wk->cand,
+           &counters = wk->counters;
     SATMI_TRY(d_off.reserve(4 * (size_t)(nclauses + 1)));
     SATMI_TRY(d_lits.reserve(4 * (size_t)std::max<int64_t>(L, 1)));
     SATMI_TRY(d_map.reserve(4 * (size_t)(maxvar + 1)));
@@ -427,8 +460,11 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
                            clauses.as<uint64_t>());
         SATMI_HIP(hipGetLastError());
     }
-    DevBuf table, flag, pos, slotv, tiles, grand;
-    EventTimer t_pairs, t_claims;
+    DevBuf &table = wk->table, &flag = wk->flag, &pos = wk->pos, &slotv = wk->slotv, &tiles = wk->tiles,
+           &grand = wk->grand;
+    EventTimer &t_pairs = wk->t_pairs, &t_claims = wk->t_claims;
+    t_pairs.reset();
+    t_claims.reset();
     g_stats = ResStats{};
     uint64_t tcap = 0;
     unsigned long long *d_count = counters.as<unsigned long long>();

@@ -72,3 +72,26 @@ def test_cdcl_drop_in_and_driver_row():
     # [[-1, -2]] loops forever in the reference (rezultat.txt's CDCL timeouts): a timeout row
     results = driver.run_solvers([[-1, -2]], [("CDCL", cdcl_solve)], timeout=1, print_fn=lambda *a: None)
     assert results["CDCL"]["output"] == "Timeout after 1 seconds"
+
+
+def test_cdcl_long_clauses_of_repeated_literals():
+    """Clauses repeating their literals many times (the reference accepts them):
+    conflict clauses longer than 2 x variables + 2 entries, the learned-literal
+    lists' old bound (csrc/cdcl.hip analyze_conflict), against the oracle."""
+    rng = random.Random(11)
+    fs = []
+    for _ in range(120):
+        n = rng.randint(2, 5)
+        f = []
+        for _ in range(rng.randint(2, 4 * n)):
+            c = [v if rng.random() < 0.5 else -v for v in rng.sample(range(1, n + 1), rng.randint(1, n))]
+            c = c * rng.randint(2, 6)   # every literal repeated: up to 6n entries
+            rng.shuffle(c)
+            f.append(c)
+        fs.append(f)
+    rs = cdcl_batch(fs, max_iter=2000)
+    for f, r in zip(fs, rs):
+        o = oracle.cdcl(f, 2000)
+        _check(r, o["result"], o["assignment"], o["var_inc"],
+               {k: o["stats"][k] for k in ("iterations", "conflicts", "decisions", "learned", "clauses",
+                                           "watch_keys", "level")})
