@@ -160,14 +160,14 @@ def _report_lines(formula, results):
     return out
 
 
-def save_results_to_file(formula, results, filename="results.txt"):
+def save_results_to_file(formula, results, filename="results.txt", print_fn=print):
     """Append the comparison report to `filename` in the reference's format (REF.py:441-487)."""
     try:
         with open(filename, "a") as fh:
             fh.writelines(_report_lines(formula, results))
-        print(f"\nResults saved to {filename} (without clause details)")
+        print_fn(f"\nResults saved to {filename} (without clause details)")
     except IOError as e:
-        print(f"Error saving file: {e}")
+        print_fn(f"Error saving file: {e}")
 
 
 def main_menu(input_fn=input, print_fn=print, solver_table=None, report_file="rezultat.txt"):
@@ -226,7 +226,7 @@ def main_menu(input_fn=input, print_fn=print, solver_table=None, report_file="re
                 continue
             results = run_solvers(formula, to_run, TIMEOUT_SECONDS, print_fn)
             if input_fn("\nSave these results to file? (y/n): ").lower() == "y":
-                save_results_to_file(formula, results, report_file)
+                save_results_to_file(formula, results, report_file, print_fn)
             print_fn("\n1. Run more solvers on same formula")
             print_fn("2. Back to main menu")
             if input_fn("Choose option: ").strip() == "2":

@@ -29,8 +29,12 @@ def test_report_matches_reference_block(tmp_path, monkeypatch, golden_dir):
         "Hybrid": {"time": 60, "memory": 31.02, "output": "Timeout after 60 seconds"},
     }
     out = tmp_path / "rezultat.txt"
-    driver.save_results_to_file(_formula_50x10(), results, str(out))
+    said = []
+    driver.save_results_to_file(_formula_50x10(), results, str(out), print_fn=said.append)
     assert out.read_text() == expected
+    assert said == [f"\nResults saved to {out} (without clause details)"]
+    driver.save_results_to_file(_formula_50x10(), results, str(tmp_path), print_fn=said.append)
+    assert said[-1].startswith("Error saving file:")
 
 
 def test_describe_result():
