@@ -79,6 +79,15 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
+// the same within each 16-lane row (enough when only lanes 0..15 hold values)
+__device__ __forceinline__ int row_incl_scan(int x) {
+    x += SATMI_DPP(0, x, DPP_ROW_SHR1, 0xf);
+    x += SATMI_DPP(0, x, DPP_ROW_SHR2, 0xf);
+    x += SATMI_DPP(0, x, DPP_ROW_SHR4, 0xf);
+    x += SATMI_DPP(0, x, DPP_ROW_SHR8, 0xf);
+    return x;
+}
+
 // inclusive prefix max over the 64 lanes
 __device__ __forceinline__ int wave_incl_max(int x) {
     x = max(x, SATMI_DPP(INT_MIN, x, DPP_ROW_SHR1, 0xf));

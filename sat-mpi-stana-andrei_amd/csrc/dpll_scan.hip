@@ -357,22 +357,26 @@ __device__ __forceinline__ int emptier(const SLds<K, C> &S, typename Pack<K>::W 
 // found at most this many of them: ranked in clause order by register
 // comparisons (no bitmap round trips through LDS).
 constexpr int FAST_UNITS = 8;
+constexpr int FAST_BATCH = 16;
 
 template <int K, typename C>
 __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t ep, uint32_t bep, int *empty_at) {
     using W = typename Pack<K>::W;
     const int ln = lane_id();
-    if (__builtin_expect(tl - rs <= 64, 1)) {
+    // fast path: a batch of at most FAST_BATCH literals (lanes 0..15; larger
+    // batches are rare and take the general path below)
+    if (__builtin_expect(tl - rs <= FAST_BATCH, 1)) {
         // lane b: the b-th batch literal's negation and its occurrence list
         // predicated (no exec-mask branch): lanes past the batch read entry rs
         const bool inb = ln < tl - rs;
         const uint32_t x = (uint32_t)S.trail[inb ? rs + ln : rs] ^ 1u;
         const int o0 = S.occ_off[x], o1 = S.occ_off[x + 1];
         const int ob = inb ? o0 : 0, len = inb ? o1 - o0 : 0;
-        const int incl = wave_incl_scan(len);
+        // the batch sits in lanes 0..15: the row scan covers it
+        const int incl = row_incl_scan(len);
         const int excl = incl - len;
         const int delta = ob - excl;
-        const int total = lane63(incl);
+        const int total = __builtin_amdgcn_readlane(incl, 15);
         if (__builtin_expect(total <= 64, 1)) {
             // one touched clause per lane
             int d = __builtin_amdgcn_readlane(delta, 0);
@@ -550,7 +554,6 @@ template <int K, bool INC, typename C>
 __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool dec, uint32_t &ep, uint32_t &props,
                           uint32_t &rounds, PhaseClock &ph) {
     const int ln = lane_id();
-    const uint64_t lt = lanemask_lt();
     int e = INT_MAX;   // set: the round that emptied a clause (handled after the loop)
     int rs = tl;
     // the decision literal (the first batch's first entry, always assigned or
@@ -563,11 +566,12 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
         int k0 = 0;
         do {   // nu > 0: at least one step
             const int k = k0 + ln;
-            const bool valid = k < nu;
-            const uint32_t code = (uint32_t)S.snap[valid ? k : 0];   // predicated loads
+            // lanes past nu read entry 0 (its variable is stamped with index 0
+            // != k: never first).  Stale entries past nu are not safe to read:
+            // an epoch can repeat across rounds, and so can (stamp, index).
+            const uint32_t code = (uint32_t)S.snap[k < nu ? k : 0];
             const uint32_t v = code >> 1;
-            // lanes past nu read entry 0, whose variable is stamped with index 0
-            // != k: never first.  (One compare: its ballot folds into the v_cmp.)
+            // (one compare: its ballot folds into the v_cmp)
 #ifdef SATMI_DUP_ASSIGN
             const bool first = (S.ts[v] | (((const volatile uint32_t *)S.ts)[v] & opaque_zero())) ==
                                stamp(bep, (uint32_t)k);
@@ -575,12 +579,11 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             const bool first = S.ts[v] == stamp(bep, (uint32_t)k);
 #endif
             const uint64_t mk = __ballot(first);
-            // predicated stores (no exec-mask branch): the other lanes write
-            // the first entry past the batch (dead: the trail is a stack, and
-            // tl + batch <= n <= ncap keeps it in the array) and re-assert the
-            // padding / dummy codes' fixed states
-            S.trail[tl + __popcll(mk & (first ? lt : ~0ull))] = (C)code;
-            lv_assign(S.lv, first ? code : CODE_DUMMY);
+            if (first) {   // trail slot: tl + the first entries on lower lanes (k order)
+                S.trail[__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mk, (uint32_t)tl))] = (C)code;
+                lv_assign(S.lv, code);
+            }
 #ifdef SATMI_DUP_ASSIGN
             {
                 const uint32_t cd = first ? code : CODE_DUMMY;
@@ -610,7 +613,7 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
         keep += __popcll(__ballot(p));
     }
     const int cut = rs + keep;
-    for (int i = cut + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
+    for (int i = cut + lane_id_here(); i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
     wave_sync();
     tl = cut;
     props += keep;   // >= 1: the batch's first entry (stamp index 0) is kept
@@ -1340,7 +1343,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
             if (top >= 0) {
                 const uint32_t fv = uniform_u32(S.fvar[top]);
                 const int ft = (int)uniform_u32(S.ftrail[top]);
-                for (int i = ft + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
+                for (int i = ft + lane_id_here(); i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
                 tl = ft;
                 ep = next_decision_epoch<K>(S, n, ep);
                 if (ln == 0) {
@@ -1366,7 +1369,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                 const uint32_t fv = uniform_u32(S.fvar[top]);   // its False branch has not run here
                 const uint32_t ftw = uniform_u32(S.ftrail[top]);
                 const int ft = (int)(ftw & ~DON);
-                for (int i = ft + ln; i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
+                for (int i = ft + lane_id_here(); i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
                 tl = ft;
                 wave_sync();
                 if (ftw & DON) {
