@@ -86,6 +86,7 @@ LEGS = [
     ("configs[4] uf250", "uf250", ["--steps", "4", "--warmup", "1"]),
     ("configs[4] 5sat-n200", "5sat-n200", ["--steps", "4", "--warmup", "1"]),
     ("cdcl", "cdcl", ["--steps", "3", "--warmup", "1"]),
+    ("cdcl 4 threads", "cdcl", ["--steps", "3", "--warmup", "1", "--threads", "4"]),
 ]
 
 
@@ -117,7 +118,7 @@ def parse(argv=None):
                    help="nodes before a search may donate (satmi_dpll_set_split_warmup; -1 = default)")
     p.add_argument("--helpers-per-cu", type=int, default=0, help="branch-splitting helpers per CU (0 = library default)")
     p.add_argument("--threads", type=int, default=1,
-                   help="php-dp: concurrent solves per step, one host thread (and HIP stream) each")
+                   help="php-dp / cdcl: concurrent solve calls per step, one host thread (and HIP stream) each")
     p.add_argument("--streams", type=int, default=None, choices=range(1, 17),
                    help="HIP streams (each with its own resident batch) the steps rotate over (default: 16 for "
                         "3sat-n50, whose 4,096 short searches leave most CU slots idle for a launch's 2 ms, else 2)")
@@ -640,47 +641,67 @@ def run_cdcl(args, world, rank, local):
     call over the preset's formulas (host arrays in, verdicts out), each run to
     its verdict or max_iter iterations (the reference's own loop is unbounded;
     its driver times it out).  Replicas across ranks."""
-    from satmi.cdcl import CDCL_LIMIT, CDCL_SAT, CDCL_UNSAT, cdcl_batch_packed
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from satmi.cdcl import CDCL_LIMIT, CDCL_SAT, CDCL_UNSAT, STAT_NAMES, cdcl_batch_packed
     torch.cuda.set_device(local)
     nf, ncl, maxlit, nvar, max_iter, seed = CDCL[args.workload]
-    hb = cnf.menu_batch(nf, ncl, maxlit, nvar, seed=seed)   # the CSR host arrays the C ABI takes
+    T = max(1, args.threads)
+    # the CSR host arrays the C ABI takes: one batch per concurrent solve
+    # (seed + thread index), thread 0's is the one checked and CPU-timed
+    hbs = [cnf.menu_batch(nf, ncl, maxlit, nvar, seed=seed + t) for t in range(T)]
+    hb = hbs[0]
+    pool_ex = ThreadPoolExecutor(T) if T > 1 else None
+
+    def step():
+        if pool_ex is None:
+            return [cdcl_batch_packed(hb, max_iter=max_iter, arrays=True)]
+        return list(pool_ex.map(lambda b: cdcl_batch_packed(b, max_iter=max_iter, arrays=True), hbs))
+
     for _ in range(0 if args.profile_steps else args.warmup):
-        cdcl_batch_packed(hb, max_iter=max_iter)
+        step()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     res = None
     for _ in range(args.steps):
-        res = cdcl_batch_packed(hb, max_iter=max_iter)
+        res = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if pool_ex is not None:
+        pool_ex.shutdown()
     el = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    st = [r["status"] for r in res]
-    iters = sum(r["stats"]["iterations"] for r in res)
-    out = {"metric": METRIC, "value": nf * args.steps * world / elapsed, "unit": "formulas/s", "n_gpus": world,
+    st = np.concatenate([r["status"] for r in res])
+    iters = int(sum(r["stats"][:, STAT_NAMES.index("iterations")].sum() for r in res))
+    out = {"metric": METRIC, "value": nf * T * args.steps * world / elapsed, "unit": "formulas/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32/f64 activities",
            "data": f"synthetic: {nf} formulas of generate_large_formula({ncl}, {maxlit}, {nvar})'s distribution "
-                   f"(REF.py:21-29; satmi.cnf.menu_batch, seed {seed})",
+                   f"per solve call (REF.py:21-29; satmi.cnf.menu_batch, seed {seed}"
+                   + (f"..{seed + T - 1}, one per concurrent call)" if T > 1 else ")"),
            "config": {"workload": f"cdcl_solve (REF.py:382-384) on {nf} formulas, <= {max_iter} iterations each; "
-                                  f"replicas across ranks", "preset": args.workload,
-                      "parallelism": f"replicas x{world}"},
-           "sat": st.count(CDCL_SAT), "unsat": st.count(CDCL_UNSAT), "iteration_capped": st.count(CDCL_LIMIT),
+                                  f"replicas across ranks"
+                                  + (f"; {T} concurrent calls per step (host threads, one HIP stream each)"
+                                     if T > 1 else ""), "preset": args.workload,
+                      "parallelism": f"replicas x{world}", "concurrent_solves": T},
+           "sat": int((st == CDCL_SAT).sum()), "unsat": int((st == CDCL_UNSAT).sum()),
+           "iteration_capped": int((st == CDCL_LIMIT).sum()),
            "iterations_per_s": iters * args.steps * world / elapsed,
            "roofline": None}
+    r0 = res[0]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         for i in range(0, nf, max(1, nf // 16)):   # verdicts checked against the oracle on a sample
             o = oracle.cdcl(hb.instance(i), max_iter=max_iter)
-            g = {CDCL_SAT: 1, CDCL_UNSAT: 0, CDCL_LIMIT: -1}.get(res[i]["status"], -2)
-            if o["result"] != g or (g == 1 and o["assignment"] != res[i]["assignment"]):
+            g = {CDCL_SAT: 1, CDCL_UNSAT: 0, CDCL_LIMIT: -1}.get(int(r0["status"][i]), -2)
+            if o["result"] != g or (g == 1 and o["assignment"] != r0["assign"][i, :r0["assign_len"][i]].tolist()):
                 raise SystemExit(f"bench: GPU and oracle disagree on CDCL formula {i}")
         pool, cores = cpu_pool("cdcl", hb.inst_clause_begin, hb.clause_lit_begin, hb.lits, args.cpu_seconds,
                                max_iter)

@@ -656,19 +656,56 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     return max_vars >= 0 && max_vars < (1 << 29);
 }
 
-// Device memory of satmi_cdcl_batch_host, kept between calls (grow-only, per
-// device): the per-wave arenas of a batch are sized for max_iter learned
-// clauses and reach gigabytes, whose hipMalloc / hipFree per call cost more
-// than the solves of a menu-sized batch.  Calls are serialised on it (each
-// call drains its stream before returning).
-struct CdclScratch {
-    std::mutex mu;
-    std::vector<std::pair<void *, size_t>> dev;   // per device: pointer, bytes
+// Device memory of satmi_cdcl_batch_host, kept between calls (grow-only): the
+// per-wave arenas of a batch are sized for max_iter learned clauses and reach
+// gigabytes, whose hipMalloc / hipFree per call cost more than the solves of a
+// menu-sized batch.  One slot per concurrent call (a call takes a free slot of
+// its device or adds one, and returns it when done), each with its own
+// non-blocking stream: calls from several host threads overlap on the device,
+// so the waves a batch's few long solves leave idle run another batch.  The
+// slots are bounded by the peak number of concurrent calls; never destroyed (no
+// hipFree after the runtime's teardown).
+struct CdclSlot {
+    int dev = 0;
+    bool busy = false;
+    void *p = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
 };
-CdclScratch &cdcl_scratch() {
-    static CdclScratch *c = new CdclScratch;   // never destroyed: no hipFree after the runtime's teardown
+struct CdclPool {
+    std::mutex mu;
+    std::vector<CdclSlot *> slots;
+};
+CdclPool &cdcl_pool() {
+    static CdclPool *c = new CdclPool;
     return *c;
 }
+// a free slot of device `dev` (created with its stream when none is free)
+CdclSlot *cdcl_acquire(int dev) {
+    CdclPool &P = cdcl_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (CdclSlot *c : P.slots)
+        if (c->dev == dev && !c->busy) {
+            c->busy = true;
+            return c;
+        }
+    CdclSlot *c = new CdclSlot;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    c->dev = dev;
+    c->busy = true;
+    P.slots.push_back(c);
+    return c;
+}
+struct CdclSlotGuard {
+    CdclSlot *c;
+    ~CdclSlotGuard() {
+        std::lock_guard<std::mutex> lk(cdcl_pool().mu);
+        c->busy = false;
+    }
+};
 
 }  // namespace
 }  // namespace satmi
@@ -745,19 +782,23 @@ extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_cl
     const size_t o_wc = o_vi + up(8 * (size_t)num_instances);
     const size_t o_arena = o_wc + 256;
     const size_t total = o_arena + (size_t)grid * (size_t)lay.bytes;
-    CdclScratch &cs = cdcl_scratch();
-    std::lock_guard<std::mutex> lk(cs.mu);
-    if ((int)cs.dev.size() <= dev) cs.dev.resize(dev + 1, {nullptr, 0});
-    auto &slot = cs.dev[dev];
-    if (slot.second < total) {
-        if (slot.first) (void)hipFree(slot.first);
-        slot = {nullptr, 0};
+    CdclSlot *slot = cdcl_acquire(dev);
+    if (!slot) {
+        set_error("satmi_cdcl_batch_host: hipStreamCreate failed");
+        return SATMI_ERR_HIP;
+    }
+    CdclSlotGuard guard{slot};
+    if (slot->cap < total) {
+        if (slot->p) (void)hipFree(slot->p);
+        slot->p = nullptr;
+        slot->cap = 0;
         void *p = nullptr;
         SATMI_HIP(hipMalloc(&p, total));
-        slot = {p, total};
+        slot->p = p;
+        slot->cap = total;
     }
-    unsigned char *d = (unsigned char *)slot.first;
-    hipStream_t s = nullptr;
+    unsigned char *d = (unsigned char *)slot->p;
+    hipStream_t s = slot->stream;
     int rc = SATMI_OK;
     do {
         auto h2d = [&](size_t off, const void *src, size_t bytes) {
@@ -790,14 +831,15 @@ extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_cl
         A.work_counter = (uint32_t *)(d + o_wc);
         hipLaunchKernelGGL(cdcl_kernel, dim3(grid), dim3(64), 0, s, A);
         hipError_t e = hipGetLastError();
+        auto d2h = [&](void *dst, size_t off, size_t bytes) {
+            if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, d + off, bytes, hipMemcpyDeviceToHost, s);
+        };
+        d2h(h_status, o_st, 4 * (size_t)num_instances);
+        d2h(h_assign_len, o_al, 4 * (size_t)num_instances);
+        d2h(h_assign, o_as, 4 * (size_t)num_instances * assign_stride);
+        d2h(h_stats, o_stats, 8 * (size_t)num_instances * SATMI_CDCL_NSTATS);
+        d2h(h_var_inc, o_vi, 8 * (size_t)num_instances);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e == hipSuccess) e = hipMemcpy(h_status, d + o_st, 4 * (size_t)num_instances, hipMemcpyDeviceToHost);
-        if (e == hipSuccess) e = hipMemcpy(h_assign_len, d + o_al, 4 * (size_t)num_instances, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && assign_stride > 0)
-            e = hipMemcpy(h_assign, d + o_as, 4 * (size_t)num_instances * assign_stride, hipMemcpyDeviceToHost);
-        if (e == hipSuccess)
-            e = hipMemcpy(h_stats, d + o_stats, 8 * (size_t)num_instances * SATMI_CDCL_NSTATS, hipMemcpyDeviceToHost);
-        if (e == hipSuccess) e = hipMemcpy(h_var_inc, d + o_vi, 8 * (size_t)num_instances, hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = hip_fail(e, "satmi_cdcl_batch_host: launch / copy back");
     } while (0);
     return rc;

@@ -28,8 +28,12 @@ def cdcl_batch(formulas, max_iter=0, time_limit=0.0, learn_cap=0):
     return cdcl_batch_packed(pack(formulas), max_iter=max_iter, time_limit=time_limit, learn_cap=learn_cap)
 
 
-def cdcl_batch_packed(batch, max_iter=0, time_limit=0.0, learn_cap=0):
-    """cdcl_batch on a CnfBatch (the CSR host arrays of include/satmi.h)."""
+def cdcl_batch_packed(batch, max_iter=0, time_limit=0.0, learn_cap=0, arrays=False):
+    """cdcl_batch on a CnfBatch (the CSR host arrays of include/satmi.h).
+    arrays=True returns the output arrays of satmi_cdcl_batch_host as they are
+    (status[B], assign_len[B], assign[B, nv], stats[B, NSTATS], var_inc[B])
+    instead of one dict per formula.  Calls from several host threads run
+    concurrently on the device (each call has its own stream and arena)."""
     L = _capi.load()
     _capi.require_gpu()
     B = batch.num_instances
@@ -45,6 +49,8 @@ def cdcl_batch_packed(batch, max_iter=0, time_limit=0.0, learn_cap=0):
                                  int(max_iter), int(learn_cap), float(time_limit), i32(status), i32(alen), i32(assign),
                                  nv, stats.ctypes.data_as(P(ctypes.c_int64)), vinc.ctypes.data_as(P(ctypes.c_double)))
     _capi.check(rc, "satmi_cdcl_batch_host")
+    if arrays:
+        return {"status": status, "assign_len": alen, "assign": assign, "stats": stats, "var_inc": vinc}
     return [{"status": int(status[b]), "assignment": assign[b, :alen[b]].tolist(),
              "stats": dict(zip(STAT_NAMES, stats[b].tolist())), "var_inc": float(vinc[b])} for b in range(B)]
 

@@ -95,3 +95,29 @@ def test_cdcl_long_clauses_of_repeated_literals():
         _check(r, o["result"], o["assignment"], o["var_inc"],
                {k: o["stats"][k] for k in ("iterations", "conflicts", "decisions", "learned", "clauses",
                                            "watch_keys", "level")})
+
+
+def test_cdcl_concurrent_calls_from_threads():
+    """satmi_cdcl_batch_host from several host threads at once (one arena and
+    stream per concurrent call): every call's outputs equal the same batch run
+    alone, in both return forms."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from satmi import cnf
+    from satmi.cdcl import cdcl_batch_packed
+    batches = [cnf.menu_batch(512, 80, 3, 15, seed=900 + t) for t in range(6)]
+    alone = [cdcl_batch_packed(b, max_iter=3000, arrays=True) for b in batches]
+    with ThreadPoolExecutor(6) as ex:
+        for _ in range(2):
+            together = list(ex.map(lambda b: cdcl_batch_packed(b, max_iter=3000, arrays=True), batches))
+            for a, t in zip(alone, together):
+                for key in ("status", "assign_len", "stats", "var_inc"):
+                    assert (a[key] == t[key]).all(), key
+                for i in range(len(a["status"])):   # models: the first assign_len entries of a row
+                    n = a["assign_len"][i]
+                    assert (a["assign"][i, :n] == t["assign"][i, :n]).all(), i
+    dicts = cdcl_batch_packed(batches[0], max_iter=3000)
+    a = alone[0]
+    for i in (0, 7, 511):
+        assert dicts[i]["status"] == a["status"][i]
+        assert dicts[i]["assignment"] == a["assign"][i, :a["assign_len"][i]].tolist()
