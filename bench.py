@@ -523,24 +523,28 @@ def dp_roofline(stats, cus, clock_hz):
             "key_words": K, "clock_hz": clock_hz}
 
 
-def saturation_roofline(stats):
+def saturation_roofline(stats, nvars):
     """Resolution (php-res): the dominant of its two kernels per step, timed by
     HIP events on the library's stream (satmi_resolution_last_stats).  Claim
-    kernel (hash dedup): per candidate its key (8K B) read, one table slot
-    read + CAS (16 B), the occupant's key compared (8K B), flag + slot written
-    (16 B); pair kernel: per pair key i read (8K B), per candidate its key
-    written (8K B); K = 2 x 64-bit words per clause for <= 64 variables."""
+    kernel (hash dedup), K = 2 x 64-bit words per clause key for <= 64
+    variables: with <= 31 variables the table holds packed one-word keys
+    (csrc/resolution.hip pack_key) -- per candidate its key read (8K B), one
+    slot read + CAS (16 B), its flag written (8 B); beyond, per candidate its
+    key (8K B), one slot read + CAS (16 B), the occupant's key compared (8K B),
+    flag + slot written (16 B).  Pair kernel: per pair key i read (8K B), per
+    candidate its key written (8K B)."""
     if not stats:
         return None
     K = 2   # PHP(4,3): 12 variables -> one word per sign
+    packed = nvars <= 31
     cand = sum(s["candidates"] for s in stats) / len(stats)
     pairs = sum(s["pairs"] for s in stats) / len(stats)
     cms = sum(s["claim_ms"] for s in stats) / len(stats)
     pms = sum(s["pair_ms"] for s in stats) / len(stats)
-    claim_b = cand * (16 * K + 32)
+    claim_b = cand * (8 * K + 24) if packed else cand * (16 * K + 32)
     pair_b = pairs * 8 * K + cand * 8 * K
-    name, b, ms = ("ht_cand_kernel (hash claims)", claim_b, cms) if cms >= pms else \
-        ("res_pairs_kernel", pair_b, pms)
+    name, b, ms = ("ht_cand_packed_kernel (hash claims)" if packed else "ht_cand_kernel (hash claims)",
+                   claim_b, cms) if cms >= pms else ("res_pairs_kernel", pair_b, pms)
     ach = b / (ms * 1e-3) / 1e9
     pmc = load_profile("pmc_traffic.json", "php-res_" + name.split()[0])
     return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
@@ -612,7 +616,7 @@ def run_saturation(args, world, rank, local):
                                      else ""),
                       "preset": args.workload, "parallelism": f"replicas x{world}", "concurrent_solves": T},
            "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
-           "roofline": saturation_roofline(stats) if args.workload == "php-res" else
+           "roofline": saturation_roofline(stats, len({abs(l) for c in f for l in c})) if args.workload == "php-res" else
            dp_roofline(stats, torch.cuda.get_device_properties(local).multi_processor_count, SHADER_CLOCK_HZ)}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:

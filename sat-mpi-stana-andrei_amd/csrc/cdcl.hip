@@ -54,6 +54,11 @@ struct CdclLayout {
     int64_t clause_cap, lit_cap, pool_cap, snap_cap;
     int32_t ncap;   // variables
     int32_t lcap;   // one learned-literal list in scratch: 2 x variables + the longest clause (repeats)
+    // the per-variable and per-key arrays ([val, pool) of the arena) and the
+    // learned-literal scratch, in the wave's LDS when they fit (lds_bytes > 0):
+    // the lane-0 watch-list adds and conflict analysis are chains of dependent
+    // reads of exactly these arrays
+    uint32_t lds_bytes, lds_scratch;
 };
 
 struct CdclArgs {
@@ -262,17 +267,25 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             const int32_t *t = S.pool + S.woff[ki];
             const int32_t mask = S.wmask[ki];
             int n = 0;
-            for (int i0 = 0; i0 <= mask; i0 += 64) {
-                const int i = i0 + ln;
-                const int32_t x = i <= mask ? t[i] : WS_EMPTY;
-                const bool act = x != WS_EMPTY && x != WS_DUMMY;
-                const uint64_t am = __ballot(act);
-                if (act) {
-                    const int p = n + __popcll(am & lt);
-                    S.snap[p] = x - 1;
-                    S.slot[p] = i;
+            for (int i0 = 0; i0 <= mask; i0 += 4 * 64) {   // four table reads in flight per step
+                int32_t xs[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + 64 * u + ln;
+                    xs[u] = i <= mask ? t[i] : WS_EMPTY;
                 }
-                n += __popcll(am);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int32_t x = xs[u];
+                    const bool act = x != WS_EMPTY && x != WS_DUMMY;
+                    const uint64_t am = __ballot(act);
+                    if (act) {
+                        const int p = n + __popcll(am & lt);
+                        S.snap[p] = x - 1;
+                        S.slot[p] = i0 + 64 * u + ln;
+                    }
+                    n += __popcll(am);
+                }
             }
             wave_sync();
             // replacement watch per snapshot clause, one clause per lane
@@ -582,27 +595,32 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
 }
 
 __global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char cdcl_lds[];
     unsigned char *base = A.arena + (size_t)blockIdx.x * (size_t)A.lay.bytes;
+    // [val, pool) of the layout, relocated into LDS when it fits
+    const auto small = [&](uint64_t off) -> unsigned char * {
+        return A.lay.lds_bytes ? cdcl_lds + (off - A.lay.val) : base + off;
+    };
     St S;
     S.coff = (int64_t *)(base + A.lay.coff);
     S.lits = (int32_t *)(base + A.lay.lits);
-    S.val = (int8_t *)(base + A.lay.val);
-    S.ord = (int64_t *)(base + A.lay.ord);
-    S.lev = (int32_t *)(base + A.lay.lev);
-    S.ante = (int64_t *)(base + A.lay.ante);
-    S.act = (double *)(base + A.lay.act);
-    S.appears = (uint64_t *)(base + A.lay.appears);
-    S.klit = (int32_t *)(base + A.lay.klit);
-    S.kidx = (int32_t *)(base + A.lay.kidx);
-    S.woff = (int64_t *)(base + A.lay.woff);
-    S.wmask = (int32_t *)(base + A.lay.wmask);
-    S.wfill = (int32_t *)(base + A.lay.wfill);
-    S.wused = (int32_t *)(base + A.lay.wused);
+    S.val = (int8_t *)small(A.lay.val);
+    S.ord = (int64_t *)small(A.lay.ord);
+    S.lev = (int32_t *)small(A.lay.lev);
+    S.ante = (int64_t *)small(A.lay.ante);
+    S.act = (double *)small(A.lay.act);
+    S.appears = (uint64_t *)small(A.lay.appears);
+    S.klit = (int32_t *)small(A.lay.klit);
+    S.kidx = (int32_t *)small(A.lay.kidx);
+    S.woff = (int64_t *)small(A.lay.woff);
+    S.wmask = (int32_t *)small(A.lay.wmask);
+    S.wfill = (int32_t *)small(A.lay.wfill);
+    S.wused = (int32_t *)small(A.lay.wused);
     S.pool = (int32_t *)(base + A.lay.pool);
     S.snap = (int32_t *)(base + A.lay.snap);
     S.rep = (int32_t *)(base + A.lay.rep);
     S.slot = (int32_t *)(base + A.lay.slot);
-    S.scratch = (int32_t *)(base + A.lay.scratch);
+    S.scratch = A.lay.lds_bytes ? (int32_t *)(cdcl_lds + A.lay.lds_scratch) : (int32_t *)(base + A.lay.scratch);
     span_begin(A.work_counter);
     for (;;) {
         uint32_t b = 0;
@@ -614,6 +632,8 @@ __global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
     }
     span_end(A.work_counter);
 }
+
+constexpr uint64_t CDCL_LDS_MAX = 32768;   // per wave (one-wave workgroups)
 
 bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int max_len, int64_t learn_cap,
                       CdclLayout *L) {
@@ -648,6 +668,9 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     L->lcap = (int32_t)std::min<int64_t>(2 * N + 2 + std::max(max_len, 1), INT32_MAX / 8);
     L->scratch = o; o = a(o + 4 * 2 * (uint64_t)L->lcap);   // two learned-literal lists
     L->bytes = o;
+    const uint64_t small = L->pool - L->val, lds = small + 4 * 2 * (uint64_t)L->lcap;
+    L->lds_bytes = lds <= CDCL_LDS_MAX ? (uint32_t)lds : 0u;
+    L->lds_scratch = (uint32_t)small;
     L->clause_cap = C;
     L->lit_cap = Lc;
     L->pool_cap = P;
@@ -829,7 +852,7 @@ extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_cl
         A.arena = d + o_arena;
         A.lay = lay;
         A.work_counter = (uint32_t *)(d + o_wc);
-        hipLaunchKernelGGL(cdcl_kernel, dim3(grid), dim3(64), 0, s, A);
+        hipLaunchKernelGGL(cdcl_kernel, dim3(grid), dim3(64), lay.lds_bytes, s, A);
         hipError_t e = hipGetLastError();
         auto d2h = [&](void *dst, size_t off, size_t bytes) {
             if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, d + off, bytes, hipMemcpyDeviceToHost, s);

@@ -242,6 +242,39 @@ __global__ void ht_cand_kernel(uint64_t *table, uint64_t mask, KeySrc S, int64_t
     }
 }
 
+// Packed table (at most 31 variables): a key (P, N) is one word P | N << 32 and
+// the table holds the keys themselves, so a probe compares in register -- no
+// second random read of the occupant's key -- and nothing is re-pointed at
+// append time.  Bit 31 of P and N is never set, so no key equals HT_EMPTY.
+__device__ __forceinline__ uint64_t pack_key(const uint64_t *x) { return x[0] | (x[1] << 32); }
+
+// 1 if key k claimed a slot (absent before), 0 if it was present
+__device__ __forceinline__ int ht_insert_packed(uint64_t *table, uint64_t mask, uint64_t k) {
+    uint64_t s = mix64(k) & mask;
+    for (;;) {
+        uint64_t cur = __hip_atomic_load(table + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == HT_EMPTY) {
+            cur = atomicCAS((unsigned long long *)(table + s), (unsigned long long)HT_EMPTY, (unsigned long long)k);
+            if (cur == HT_EMPTY) return 1;
+        }
+        if (cur == k) return 0;
+        s = (s + 1) & mask;
+    }
+}
+
+__global__ void ht_clauses_packed_kernel(uint64_t *table, uint64_t mask, const uint64_t *clauses, int64_t c0,
+                                         int64_t c1) {
+    for (int64_t c = c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < c1; c += (int64_t)gridDim.x * blockDim.x)
+        (void)ht_insert_packed(table, mask, pack_key(clauses + 2 * c));
+}
+
+__global__ void ht_cand_packed_kernel(uint64_t *table, uint64_t mask, const uint64_t *cand, int64_t n,
+                                      int64_t *flag) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        flag[t] = ht_insert_packed(table, mask, pack_key(cand + 2 * t));
+    }
+}
+
 // clauses.extend(new): the claimed candidates become clauses first .. first +
 // count, in append order; their table entries are re-pointed at the clause
 // array (the candidate buffer is reused by the next chunk)
@@ -251,7 +284,7 @@ __global__ void res_append_kernel(const uint64_t *cand, const int64_t *flag, con
         if (!flag[t]) continue;
         const int64_t c = first + pos[t];
         for (int w = 0; w < K; ++w) clauses[c * K + w] = cand[t * K + w];
-        __hip_atomic_store(table + slot[t], (uint64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (table) __hip_atomic_store(table + slot[t], (uint64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -434,6 +467,7 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
     const int V = (int)dense2var.size();
     const int W = std::max(1, (V + 63) / 64);
     const int K = 2 * W;
+    const bool packed = V <= 31;   // the packed table (see pack_key)
     const int64_t slot_base = g_slot_base;
     int dev_id = 0;
     SATMI_HIP(hipGetDevice(&dev_id));
@@ -474,7 +508,10 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
         tcap = table_slots(room);
         SATMI_TRY(table.reserve(8 * tcap));
         SATMI_HIP(hipMemsetAsync(table.p, 0xFF, 8 * tcap, s));   // HT_EMPTY
-        if (nkeys > 0)
+        if (nkeys > 0 && packed)
+            hipLaunchKernelGGL(ht_clauses_packed_kernel, dim3(grid_for(nkeys)), dim3(PRIM_BLOCK), 0, s,
+                               table.as<uint64_t>(), tcap - 1, clauses.as<uint64_t>(), (int64_t)0, nkeys);
+        else if (nkeys > 0)
             hipLaunchKernelGGL(ht_clauses_kernel, dim3(grid_for(nkeys)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(),
                                tcap - 1, KeySrc{clauses.as<uint64_t>(), nullptr, 0, K}, (int64_t)0, nkeys);
         SATMI_HIP(hipGetLastError());
@@ -573,9 +610,13 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
             SATMI_TRY(tiles.reserve(8 * (size_t)((nc + SCAN_TILE - 1) / SCAN_TILE + 1)));
             SATMI_TRY(grand.reserve(8));
             t_claims.begin(s);
-            hipLaunchKernelGGL(ht_cand_kernel, dim3(grid_for(nc)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(),
-                               tcap - 1, KeySrc{clauses.as<uint64_t>(), cand.as<uint64_t>(), slot_base, K}, nc,
-                               flag.as<int64_t>(), slotv.as<int64_t>());
+            if (packed)
+                hipLaunchKernelGGL(ht_cand_packed_kernel, dim3(grid_for(nc)), dim3(PRIM_BLOCK), 0, s,
+                                   table.as<uint64_t>(), tcap - 1, cand.as<uint64_t>(), nc, flag.as<int64_t>());
+            else
+                hipLaunchKernelGGL(ht_cand_kernel, dim3(grid_for(nc)), dim3(PRIM_BLOCK), 0, s, table.as<uint64_t>(),
+                                   tcap - 1, KeySrc{clauses.as<uint64_t>(), cand.as<uint64_t>(), slot_base, K}, nc,
+                                   flag.as<int64_t>(), slotv.as<int64_t>());
             t_claims.end(s);
             g_stats.candidates += nc;
             SATMI_HIP(hipGetLastError());
@@ -588,7 +629,7 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
             SATMI_TRY(grow_clauses(ncl + nnew + nwin));
             hipLaunchKernelGGL(res_append_kernel, dim3(grid_for(nc)), dim3(PRIM_BLOCK), 0, s, cand.as<uint64_t>(),
                                flag.as<int64_t>(), pos.as<int64_t>(), slotv.as<int64_t>(), nc, K,
-                               clauses.as<uint64_t>(), ncl + nnew, table.as<uint64_t>());
+                               clauses.as<uint64_t>(), ncl + nnew, packed ? nullptr : table.as<uint64_t>());
             SATMI_HIP(hipGetLastError());
             nnew += nwin;
         }

@@ -102,3 +102,21 @@ def test_deadline_inside_a_pass():
     assert r["result"] == -1 and r["passes"] >= 4, r
     assert r["pass_new"][:4] == [36, 270, 7132, 163954]
     assert dt < 10.0, dt
+
+
+@pytest.mark.parametrize("nvars", [31, 32, 33, 70])
+def test_table_forms_around_31_variables(nvars):
+    """Up to 31 distinct variables the dedup table holds packed keys (one word,
+    compared in register); beyond, clause / candidate indices whose keys are
+    compared in memory (and 2 words per sign past 64).  Both forms add exactly
+    the oracle's clause sets, on formulas that use every variable."""
+    rng = random.Random(nvars)
+    for _ in range(4):
+        vs = list(range(1, nvars + 1))
+        rng.shuffle(vs)
+        f = [[v if rng.random() < 0.5 else -v for v in vs[i:i + 3]] for i in range(0, nvars, 3)]
+        f += [[v if rng.random() < 0.5 else -v for v in rng.sample(range(1, nvars + 1), 2)] for _ in range(nvars // 2)]
+        o = oracle.resolution(f, record=True, max_passes=3)
+        r = resolve(f, record=True, max_passes=3)
+        assert r["result"] == o["result"] and r["pass_new"] == o["pass_new"], f
+        assert [sorted(p) for p in r["clauses"]] == [sorted(p) for p in o["clauses"]], f
