@@ -88,7 +88,28 @@ struct St {   // views into one wave's arena
     int64_t *woff;
     int32_t *wmask, *wfill, *wused;
     int32_t *pool, *snap, *rep, *slot, *scratch;
+#ifdef SATMI_CDCL_PHASES
+    uint64_t *clk;   // diagnostic build: per-phase shader clocks (lane 0), [7] = last stamp
+#endif
 };
+
+// Diagnostic build only (make variant VFLAGS=-DSATMI_CDCL_PHASES): per-phase
+// clocks of a solve written over stats[4..7] (snapshot, replacement watches,
+// watch-list moves, everything between propagate calls).
+#ifdef SATMI_CDCL_PHASES
+#define CDCL_CLK(S, i)                                             \
+    do {                                                           \
+        if (lane_id() == 0) {                                      \
+            const uint64_t _t = __builtin_amdgcn_s_memtime();      \
+            (S).clk[i] += _t - (S).clk[7];                         \
+            (S).clk[7] = _t;                                       \
+        }                                                          \
+    } while (0)
+#else
+#define CDCL_CLK(S, i) \
+    do {               \
+    } while (0)
+#endif
 
 __device__ __forceinline__ int iabs(int x) { return x < 0 ? -x : x; }
 __device__ __forceinline__ int lcode(int lit) { return (iabs(lit) << 1) | (lit < 0 ? 1 : 0); }
@@ -254,6 +275,7 @@ __device__ void sync_seq(Seq &q) {
 __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
+    CDCL_CLK(S, 3);
     const int nk0 = q.nk;   // list(self.watch_list): keys created during the pass are not visited
     for (int k0 = 0; k0 < nk0; k0 += 64) {
         const int kk = k0 + ln;
@@ -288,6 +310,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                 }
             }
             wave_sync();
+            CDCL_CLK(S, 0);
             // replacement watch per snapshot clause, one clause per lane
             int64_t conflict = -1;
             int upto = n;   // snapshot entries whose watch moves (before the conflict)
@@ -321,6 +344,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             conflict = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)conflict) |
                        ((int64_t)__builtin_amdgcn_readfirstlane((int)(conflict >> 32)) << 32);
             upto = __builtin_amdgcn_readfirstlane(upto);
+            CDCL_CLK(S, 1);
             // self.watch_list[lit].remove(idx): dummies at the snapshot's slots
             int32_t *tw = S.pool + S.woff[ki];
             for (int p = ln; p < upto; p += 64) tw[S.slot[p]] = WS_DUMMY;
@@ -330,6 +354,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                 for (int p = 0; p < upto && !q.full; ++p) watch_add(A, S, q, S.rep[p], S.snap[p]);
             }
             sync_seq(q);
+            CDCL_CLK(S, 2);
             if (conflict >= 0 || q.full) return conflict;
         }
     }
@@ -472,6 +497,12 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
     }
     sync_seq(q);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#ifdef SATMI_CDCL_PHASES
+    if (ln == 0) {
+        for (int i = 0; i < 7; ++i) S.clk[i] = 0;
+        S.clk[7] = __builtin_amdgcn_s_memtime();
+    }
+#endif
     int64_t it = 0, conflicts = 0, decisions = 0, learned = 0;
     while (!q.full) {
         if (A.max_iter > 0 && it >= A.max_iter) break;
@@ -590,6 +621,9 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
         st[5] = q.nk;
         st[6] = q.level;
         st[7] = q.pool_top;
+#ifdef SATMI_CDCL_PHASES
+        for (int i = 0; i < 4; ++i) st[4 + i] = (int64_t)S.clk[i];
+#endif
         A.var_inc[b] = q.var_inc;
     }
 }
@@ -620,6 +654,10 @@ __global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
     S.snap = (int32_t *)(base + A.lay.snap);
     S.rep = (int32_t *)(base + A.lay.rep);
     S.slot = (int32_t *)(base + A.lay.slot);
+#ifdef SATMI_CDCL_PHASES
+    __shared__ uint64_t clk_s[8];
+    S.clk = clk_s;
+#endif
     S.scratch = A.lay.lds_bytes ? (int32_t *)(cdcl_lds + A.lay.lds_scratch) : (int32_t *)(base + A.lay.scratch);
     span_begin(A.work_counter);
     for (;;) {
