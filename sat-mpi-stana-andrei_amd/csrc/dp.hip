@@ -140,8 +140,13 @@ __global__ void __launch_bounds__(256) dp_pop_kernel(const unsigned long long *f
 }
 
 // split flags (REF.py:106-108)
-__global__ void dp_split_kernel(ClauseList L, int64_t n, int W, int d, int64_t *fpos, int64_t *fneg, int64_t *frem) {
+// Also the largest image (`used`) among the clauses holding var / -var into
+// mx[0] / mx[1] (zeroed by the host): the capacities of the step's images,
+// read back with the split counts instead of after the filter.
+__global__ void dp_split_kernel(ClauseList L, int64_t n, int W, int d, int64_t *fpos, int64_t *fneg, int64_t *frem,
+                                unsigned long long *mx) {
     const int K = 2 * W;
+    int up = 0, un = 0;
     for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t *k = L.bits + c * K;
         const bool p = (k[d >> 6] >> (d & 63)) & 1ull;
@@ -149,17 +154,21 @@ __global__ void dp_split_kernel(ClauseList L, int64_t n, int W, int d, int64_t *
         fpos[c] = p;
         fneg[c] = q;
         frem[c] = !p && !q;
+        const int u = (p || q) ? L.used[c] : 0;
+        up = p ? max(up, u) : up;
+        un = q ? max(un, u) : un;
+    }
+    up = wave_max_i32(up);   // every lane reaches here (grid-stride loop)
+    un = wave_max_i32(un);
+    if (lane_id() == 0) {
+        if (up) atomicMax(mx, (unsigned long long)up);
+        if (un) atomicMax(mx + 1, (unsigned long long)un);
     }
 }
 
 __global__ void dp_compact_kernel(const int64_t *flag, const int64_t *pos, int64_t n, int64_t *out) {
     for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
         if (flag[c]) out[pos[c]] = c;
-}
-
-__global__ void dp_maxused_kernel(ClauseList L, const int64_t *idx, int64_t n, unsigned long long *mx) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
-        atomicMax(mx, (unsigned long long)L.used[idx[t]]);
 }
 
 struct Images {   // per-entry images built into 2*cap slots each
@@ -477,13 +486,15 @@ struct DpWork {
     Img A, B, R;
     std::vector<hipEvent_t> ev;   // subsumption-filter timing: one pair per step, read once per call
     hipStream_t stream = nullptr;
+    int64_t *pin = nullptr;       // pinned host word: a step's pool size, read after the next step's first wait
 };
 DpWork *dp_work(int dev) {
     thread_local std::vector<DpWork *> mine;
     if ((int)mine.size() <= dev) mine.resize(dev + 1, nullptr);
     if (!mine[dev]) {
         DpWork *w = new DpWork;
-        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc((void **)&w->pin, 64, hipHostMallocDefault) != hipSuccess) {
             delete w;
             return nullptr;
         }
@@ -590,9 +601,12 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     DP_TRY(misc.need(64));
     int cur = 0;
     int64_t ncl = nclauses;
+    int64_t pool_cur = 0;         // pool slots of g[cur] (exact, or this step's bound until read back)
+    bool pool_pending = false;    // Wk.pin[0] holds g[cur]'s exact pool size after the next wait
     {
         const int64_t cap0 = cap_for(maxlen);
-        DP_TRY(g[0].reserve(ncl, K, ncl * 2 * cap0));
+        pool_cur = ncl * 2 * cap0;
+        DP_TRY(g[0].reserve(ncl, K, pool_cur));
         if (nclauses > 0) {
             SATMI_HIP(hipMemcpyAsync(d_off.p, h_clause_off, 4 * (size_t)(nclauses + 1), hipMemcpyHostToDevice, s));
             if (Ltot) SATMI_HIP(hipMemcpyAsync(d_lits.p, h_lits, 4 * (size_t)Ltot, hipMemcpyHostToDevice, s));
@@ -658,6 +672,10 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             set_error("satmi_dp_host: set model table overflow");
             return SATMI_ERR_TOO_LARGE;
         }
+        if (pool_pending) {   // the previous step's exact pool size, copied behind its assembly
+            pool_cur = Wk.pin[0];
+            pool_pending = false;
+        }
         if (pop[1] == 0) break;   // `while variables` ends: True (REF.py:130)
         if (step_limit > 0 && steps >= step_limit) {
             result = -1;
@@ -676,8 +694,10 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         DP_TRY(fpos.need(8 * (size_t)ncl));
         DP_TRY(fneg.need(8 * (size_t)ncl));
         DP_TRY(frem.need(8 * (size_t)ncl));
+        unsigned long long *d_mx = (unsigned long long *)(misc.as<char>() + 48);
+        SATMI_HIP(hipMemsetAsync(d_mx, 0, 16, s));
         hipLaunchKernelGGL(dp_split_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, Lc, ncl, W, d,
-                           fpos.as<int64_t>(), fneg.as<int64_t>(), frem.as<int64_t>());
+                           fpos.as<int64_t>(), fneg.as<int64_t>(), frem.as<int64_t>(), d_mx);
         // the three lists with one count read-back
         DP_TRY(counts3.need(3 * sizeof(int64_t)));
         int64_t *c3 = counts3.as<int64_t>();
@@ -685,7 +705,9 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         DP_TRY(compact_deferred(fneg.as<int64_t>(), ncl, scanpos, tiles, c3 + 1, nlist, s));
         DP_TRY(compact_deferred(frem.as<int64_t>(), ncl, scanpos, tiles, c3 + 2, rlist, s));
         int64_t h3[3] = {0, 0, 0};
+        unsigned long long mx[2] = {0, 0};
         SATMI_HIP(hipMemcpyAsync(h3, c3, sizeof(h3), hipMemcpyDeviceToHost, s));
+        SATMI_HIP(hipMemcpyAsync(mx, d_mx, sizeof(mx), hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
         const int64_t np = h3[0], nn = h3[1], nr = h3[2];
         const int64_t npairs = np * nn;
@@ -772,15 +794,7 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             DP_TRY(compact(kept.as<int64_t>(), m, kpos, tiles, grand, klist, &nkept, s));
         }
         if (nkept > 0) {
-            // images of AX, BY and the kept resolvents
-            unsigned long long mx[2] = {0, 0};
-            SATMI_HIP(hipMemsetAsync(misc.as<char>() + 48, 0, 16, s));
-            hipLaunchKernelGGL(dp_maxused_kernel, dim3(grid_for(np)), dim3(PRIM_BLOCK), 0, s, Lc, plist.as<int64_t>(),
-                               np, (unsigned long long *)(misc.as<char>() + 48));
-            hipLaunchKernelGGL(dp_maxused_kernel, dim3(grid_for(nn)), dim3(PRIM_BLOCK), 0, s, Lc, nlist.as<int64_t>(),
-                               nn, (unsigned long long *)(misc.as<char>() + 56));
-            SATMI_HIP(hipMemcpyAsync(mx, misc.as<char>() + 48, 16, hipMemcpyDeviceToHost, s));
-            SATMI_HIP(hipStreamSynchronize(s));
+            // images of AX, BY and the kept resolvents (capacities from the split's mx)
             DP_TRY(A.reserve(np, cap_for((int64_t)mx[0])));
             DP_TRY(B.reserve(nn, cap_for((int64_t)mx[1])));
             DP_TRY(R.reserve(nkept, cap_for((int64_t)mx[0] + (int64_t)mx[1])));
@@ -804,15 +818,22 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             DP_TRY(tiles.need(8 * (size_t)((ncl2 + SCAN_TILE - 1) / SCAN_TILE + 1)));
             DP_TRY(exclusive_scan(sizes.as<int64_t>(), offs.as<int64_t>(), ncl2, tiles.as<int64_t>(),
                                   grand.as<int64_t>(), s));
-            SATMI_HIP(hipMemcpyAsync(&pool2, grand.p, 8, hipMemcpyDeviceToHost, s));
-            SATMI_HIP(hipStreamSynchronize(s));
+            // the next generation's pool: reserved for a bound (the remaining
+            // clauses' tables are regions of g[cur]'s pool; a kept resolvent's
+            // image has <= 2 x R.cap slots), the exact size copied back behind
+            // the assembly and read after the next step's first wait (no wait
+            // here; recording reads it at once)
+            const int64_t pool_ub = pool_cur + nkept * 2 * R.cap;
+            SATMI_HIP(hipMemcpyAsync(Wk.pin, grand.p, 8, hipMemcpyDeviceToHost, s));
             const int nxt = cur ^ 1;
-            DP_TRY(g[nxt].reserve(ncl2, K, pool2));
+            DP_TRY(g[nxt].reserve(ncl2, K, pool_ub));
             hipLaunchKernelGGL(dp_assemble_kernel, dim3(grid_for(ncl2)), dim3(PRIM_BLOCK), 0, s, Lc,
                                rlist.as<int64_t>(), nr, R.view(), klist.as<int64_t>(), nkept, rbits.as<uint64_t>(),
                                ntlist.as<int64_t>(), offs.as<int64_t>(), K, g[nxt].view());
             SATMI_HIP(hipGetLastError());
             cur = nxt;
+            pool_cur = pool_ub;
+            pool_pending = true;
         }
         ncl = ncl2;
         // record the clause list after the step, each clause in its set iteration order
@@ -821,6 +842,9 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             h_mask.resize((size_t)std::max<int64_t>(ncl, 1));
             h_pool.resize((size_t)std::max<int64_t>(pool2, 1));
             if (ncl > 0) {
+                SATMI_HIP(hipStreamSynchronize(s));   // Wk.pin[0] = pool2
+                pool2 = Wk.pin[0];
+                h_pool.resize((size_t)std::max<int64_t>(pool2, 1));
                 SATMI_HIP(hipMemcpyAsync(h_off.data(), g[cur].off.p, 8 * (size_t)ncl, hipMemcpyDeviceToHost, s));
                 SATMI_HIP(hipMemcpyAsync(h_mask.data(), g[cur].mask.p, 4 * (size_t)ncl, hipMemcpyDeviceToHost, s));
                 SATMI_HIP(hipMemcpyAsync(h_pool.data(), g[cur].pool.p, 4 * (size_t)pool2, hipMemcpyDeviceToHost, s));
