@@ -121,3 +121,24 @@ def test_cdcl_concurrent_calls_from_threads():
     for i in (0, 7, 511):
         assert dicts[i]["status"] == a["status"][i]
         assert dicts[i]["assignment"] == a["assign"][i, :a["assign_len"][i]].tolist()
+
+
+def test_cdcl_arena_form_beyond_lds():
+    """Formulas whose per-variable / per-key arrays exceed the LDS budget
+    (csrc/cdcl.hip CDCL_LDS_MAX: ~85 B per variable, so > ~380 variables) run
+    with those arrays in the HBM arena; a batch mixing them with small formulas
+    (the launch takes the arena form for all) equals the oracle."""
+    rng = random.Random(5)
+    fs = []
+    for n in (420, 600, 12, 9):
+        f = []
+        for _ in range(int(2.0 * n)):
+            c = [v if rng.random() < 0.5 else -v for v in rng.sample(range(1, n + 1), 3)]
+            f.append(c)
+        fs.append(f)
+    rs = cdcl_batch(fs, max_iter=400)
+    for f, r in zip(fs, rs):
+        o = oracle.cdcl(f, 400)
+        _check(r, o["result"], o["assignment"], o["var_inc"],
+               {k: o["stats"][k] for k in ("iterations", "conflicts", "decisions", "learned", "clauses",
+                                           "watch_keys", "level")})
