@@ -285,12 +285,20 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             const int ki = k0 + __builtin_ctzll(fm);
             fm &= fm - 1;
             const int lit = S.klit[ki];
-            // snapshot of the set in iteration order (table slot order), with slots
+            // snapshot of the set in iteration order (table slot order), with
+            // slots, taken a window of 256 slots at a time: the replacement
+            // watches of a window's members are found before the next window
+            // is read, so a conflict ends the snapshot too (REF.py's loop
+            // returns at the first clause without a replacement; the members
+            // after it are never visited)
             const int32_t *t = S.pool + S.woff[ki];
             const int32_t mask = S.wmask[ki];
             int n = 0;
-            for (int i0 = 0; i0 <= mask; i0 += 4 * 64) {   // four table reads in flight per step
-                int32_t xs[4];
+            int64_t conflict = -1;
+            int upto = -1;   // snapshot entries whose watch moves (before the conflict)
+            for (int i0 = 0; i0 <= mask && upto < 0; i0 += 4 * 64) {
+                const int n0 = n;
+                int32_t xs[4];   // four table reads in flight
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int i = i0 + 64 * u + ln;
@@ -308,38 +316,38 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                     }
                     n += __popcll(am);
                 }
-            }
-            wave_sync();
-            CDCL_CLK(S, 0);
-            // replacement watch per snapshot clause, one clause per lane
-            int64_t conflict = -1;
-            int upto = n;   // snapshot entries whose watch moves (before the conflict)
-            for (int p0 = 0; p0 < n; p0 += 64) {
-                const int p = p0 + ln;
-                int r = 0;
-                bool none = false;
-                if (p < n) {
-                    const int64_t c = S.snap[p];
-                    const int64_t jb = S.coff[c], je = S.coff[c + 1];
-                    for (int64_t j = jb; j < je; ++j) {
-                        const int o = S.lits[j];
-                        if (o == lit) continue;
-                        const int8_t v = S.val[iabs(o)];
-                        if (v < 0 || (o > 0) == (v != 0)) {
-                            r = o;
-                            break;
+                wave_sync();
+                CDCL_CLK(S, 0);
+                // replacement watch per snapshot clause, one clause per lane
+                for (int p0 = n0; p0 < n; p0 += 64) {
+                    const int p = p0 + ln;
+                    int r = 0;
+                    bool none = false;
+                    if (p < n) {
+                        const int64_t c = S.snap[p];
+                        const int64_t jb = S.coff[c], je = S.coff[c + 1];
+                        for (int64_t j = jb; j < je; ++j) {
+                            const int o = S.lits[j];
+                            if (o == lit) continue;
+                            const int8_t v = S.val[iabs(o)];
+                            if (v < 0 || (o > 0) == (v != 0)) {
+                                r = o;
+                                break;
+                            }
                         }
+                        none = r == 0;
+                        S.rep[p] = r;
                     }
-                    none = r == 0;
-                    S.rep[p] = r;
+                    const uint64_t nm = __ballot(none);
+                    if (nm) {
+                        upto = p0 + __builtin_ctzll(nm);
+                        conflict = S.snap[upto];
+                        break;
+                    }
                 }
-                const uint64_t nm = __ballot(none);
-                if (nm) {
-                    upto = p0 + __builtin_ctzll(nm);
-                    conflict = S.snap[upto];
-                    break;
-                }
+                CDCL_CLK(S, 1);
             }
+            if (upto < 0) upto = n;
             wave_sync();
             conflict = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)conflict) |
                        ((int64_t)__builtin_amdgcn_readfirstlane((int)(conflict >> 32)) << 32);
