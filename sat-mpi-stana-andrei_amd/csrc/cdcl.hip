@@ -286,7 +286,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             fm &= fm - 1;
             const int lit = S.klit[ki];
             // snapshot of the set in iteration order (table slot order), with
-            // slots, taken a window of 256 slots at a time: the replacement
+            // slots, taken a window of 64, then 256 slots at a time: the replacement
             // watches of a window's members are found before the next window
             // is read, so a conflict ends the snapshot too (REF.py's loop
             // returns at the first clause without a replacement; the members
@@ -296,13 +296,13 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             int n = 0;
             int64_t conflict = -1;
             int upto = -1;   // snapshot entries whose watch moves (before the conflict)
-            for (int i0 = 0; i0 <= mask && upto < 0; i0 += 4 * 64) {
+            for (int i0 = 0, nch = 1; i0 <= mask && upto < 0; i0 += 64 * nch, nch = 4) {
                 const int n0 = n;
-                int32_t xs[4];   // four table reads in flight
+                int32_t xs[4];   // up to four table reads in flight (the first window: one)
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int i = i0 + 64 * u + ln;
-                    xs[u] = i <= mask ? t[i] : WS_EMPTY;
+                    xs[u] = (u < nch && i <= mask) ? t[i] : WS_EMPTY;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
