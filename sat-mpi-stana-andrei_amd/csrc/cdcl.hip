@@ -369,73 +369,99 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
     return -1;
 }
 
-// analyze_conflict (REF.py:306-345) on lane 0: learned literals into S.scratch
-// (returns their count), the backtrack level into *bt; -1 where the reference
-// raises KeyError (an unassigned variable reaching self.levels[...]); -2 if a
-// list would pass `cap` entries (the arena is full: CD_FULL).  A list holds
-// distinct literals plus the repeats of the conflict clause, so cap = 2 x
-// variables + the longest clause is never reached.
+// analyze_conflict (REF.py:306-345) across the wave: learned literals into
+// S.scratch (returns their count, the same on every lane), the backtrack level
+// into *bt; -1 where the reference raises KeyError (an unassigned variable
+// reaching self.levels[...]); -2 if a list would pass `cap` entries (the arena
+// is full: CD_FULL).  A list holds distinct literals plus the repeats of the
+// conflict clause, so cap = 2 x variables + the longest clause is never
+// reached.  Each resolution step keeps REF.py's list order: the kept literals
+// in order, then the antecedent's literals in order that are not -last_lit,
+// not among the kept ones and not a repeat of an earlier antecedent literal
+// (a repeat is excluded exactly when its first occurrence was: same value,
+// same tests) -- every membership test runs on the lanes in parallel.
 __device__ int analyze_conflict(const St &S, int64_t conflict, int32_t cap, int32_t *bt) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
     const int64_t jb = S.coff[conflict], je = S.coff[conflict + 1];
-    int32_t *L = S.scratch;
-    int n = 0;
     if (je - jb > cap) return -2;
-    for (int64_t j = jb; j < je; ++j) {
-        if (S.val[iabs(S.lits[j])] < 0) return -1;
-        L[n++] = S.lits[j];
+    int32_t *L = S.scratch, *N = S.scratch + cap;
+    int n = (int)(je - jb);
+    bool bad = false;
+    for (int i = ln; i < n; i += 64) {
+        const int x = S.lits[jb + i];
+        bad |= S.val[iabs(x)] < 0;
+        L[i] = x;
     }
+    if (__ballot(bad)) return -1;
+    wave_sync();
     for (;;) {
-        int mx = -1, sc = -1, d = 0;
-        for (int i = 0; i < n; ++i) {
+        // max(levels) and max(levels - {max}) (-1: one level)
+        int mx = -1;
+        for (int i = ln; i < n; i += 64) mx = max(mx, S.lev[iabs(L[i])]);
+        mx = wave_max_i32(mx);
+        int sc = -1;
+        for (int i = ln; i < n; i += 64) {
             const int l = S.lev[iabs(L[i])];
-            bool seen = false;
-            for (int j = 0; j < i; ++j) seen |= S.lev[iabs(L[j])] == l;
-            if (seen) continue;
-            ++d;
-            if (l > mx) {
-                sc = mx;
-                mx = l;
-            } else if (l > sc) {
-                sc = l;
-            }
+            if (l < mx) sc = max(sc, l);
         }
-        bool stop = d <= 1;
-        int last = 0;
-        if (!stop) {
-            for (int i = 0; i < n; ++i)
-                if (S.lev[iabs(L[i])] == mx) {
-                    last = L[i];
-                    break;
-                }
-            stop = last == 0 || S.ante[iabs(last)] < 0;   // None or -1
-        }
-        if (stop) {
-            *bt = d > 1 ? sc : 0;
+        sc = wave_max_i32(sc);
+        if (sc < 0) {   // len(levels) <= 1
+            *bt = 0;
             return n;
         }
-        // resolve with the antecedent (REF.py:331-342): new list in scratch + cap
-        const int64_t a = S.ante[iabs(last)];
-        const int64_t ab = S.coff[a], ae = S.coff[a + 1];
-        int32_t *N = L + cap;
-        int m = 0;
-        for (int i = 0; i < n; ++i) {
-            bool neg_in = false;
-            for (int64_t j = ab; j < ae; ++j) neg_in |= S.lits[j] == -L[i];
-            if (L[i] != last && !neg_in) N[m++] = L[i];   // m <= n <= cap
-        }
-        for (int64_t j = ab; j < ae; ++j) {
-            const int x = S.lits[j];
-            bool in_new = false;
-            for (int i = 0; i < m; ++i) in_new |= N[i] == x;
-            if (x != -last && !in_new) {
-                if (m >= cap) return -2;
-                N[m++] = x;
+        // the first literal at the maximal level
+        int last = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + ln;
+            const uint64_t m = __ballot(i < n && S.lev[iabs(L[i < n ? i : 0])] == mx);
+            if (m) {
+                last = L[i0 + __builtin_ctzll(m)];
+                break;
             }
         }
-        for (int i = 0; i < m; ++i) {
-            if (S.val[iabs(N[i])] < 0) return -1;
-            L[i] = N[i];
+        const int64_t a = S.ante[iabs(last)];
+        if (a < 0) {   // None or -1
+            *bt = sc;
+            return n;
         }
+        // resolve with the antecedent (REF.py:331-342): new list at scratch + cap
+        const int64_t ab = S.coff[a], ae = S.coff[a + 1];
+        const int alen = (int)(ae - ab);
+        int m = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {   // kept literals, in order (m <= n <= cap)
+            const int i = i0 + ln;
+            const int x = i < n ? L[i] : 0;
+            bool neg_in = false;
+            for (int j = 0; j < alen; ++j) neg_in |= S.lits[ab + j] == -x;
+            const bool keep = i < n && x != last && !neg_in;
+            const uint64_t km = __ballot(keep);
+            if (keep) N[m + __popcll(km & lt)] = x;
+            m += __popcll(km);
+        }
+        wave_sync();
+        const int m1 = m;
+        for (int j0 = 0; j0 < alen; j0 += 64) {   // then the antecedent's new literals, in order
+            const int j = j0 + ln;
+            const int x = j < alen ? S.lits[ab + j] : 0;
+            bool inc = j < alen && x != -last;
+            for (int k = 0; k < m1; ++k) inc &= N[k] != x;
+            const int kend = min(alen, j0 + 64);
+            for (int k = 0; k < kend; ++k) inc &= !(k < j && S.lits[ab + k] == x);
+            const uint64_t im = __ballot(inc);
+            if (m + __popcll(im) > cap) return -2;
+            if (inc) N[m + __popcll(im & lt)] = x;
+            m += __popcll(im);
+        }
+        wave_sync();
+        bad = false;
+        for (int i = ln; i < m; i += 64) {
+            const int x = N[i];
+            bad |= S.val[iabs(x)] < 0;
+            L[i] = x;
+        }
+        if (__ballot(bad)) return -1;
+        wave_sync();
         n = m;
     }
 }
@@ -524,9 +550,9 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
                 break;
             }
             ++conflicts;
-            int32_t cnt = 0, bt = 0;
+            int32_t bt = 0;
+            int32_t cnt = analyze_conflict(S, conflict, A.lay.lcap, &bt);   // the whole wave
             if (ln == 0) {
-                cnt = analyze_conflict(S, conflict, A.lay.lcap, &bt);
                 if (cnt > 0) {   // learn_clause (REF.py:347-357)
                     if (q.nf + 1 > A.lay.clause_cap || q.nlits + cnt > A.lay.lit_cap) {
                         q.full = true;
