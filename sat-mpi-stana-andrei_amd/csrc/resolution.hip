@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -391,13 +392,15 @@ struct ResWork {
     DevBuf d_off, d_lits, d_map, clauses, cand, counters, table, flag, pos, slotv, tiles, grand;
     EventTimer t_pairs, t_claims;
     hipStream_t stream = nullptr;
+    unsigned long long *pin = nullptr;   // pinned host words: the per-chunk counters and claim count
 };
 ResWork *res_work(int dev) {
     thread_local std::vector<ResWork *> mine;
     if ((int)mine.size() <= dev) mine.resize(dev + 1, nullptr);
     if (!mine[dev]) {
         ResWork *w = new ResWork;
-        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc((void **)&w->pin, 64, hipHostMallocDefault) != hipSuccess) {
             delete w;
             return nullptr;
         }
@@ -584,13 +587,15 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
             for (int attempt = 0;; ++attempt) {
                 const int64_t cap = (int64_t)(cand.cap / (8 * (size_t)K));
                 hc = {(unsigned long long)slot_base, 0, 0};
-                SATMI_HIP(hipMemcpyAsync(counters.p, &hc, 16, hipMemcpyHostToDevice, s));
+                std::memcpy(wk->pin, &hc, 16);   // staged in pinned memory: a truly asynchronous copy
+                SATMI_HIP(hipMemcpyAsync(counters.p, wk->pin, 16, hipMemcpyHostToDevice, s));
                 t_pairs.begin(s);
                 launch_pairs(j0, j1, cap);
                 t_pairs.end(s);
                 SATMI_HIP(hipGetLastError());
-                SATMI_HIP(hipMemcpyAsync(&hc, counters.p, 16, hipMemcpyDeviceToHost, s));
+                SATMI_HIP(hipMemcpyAsync(wk->pin, counters.p, 16, hipMemcpyDeviceToHost, s));
                 SATMI_HIP(hipStreamSynchronize(s));
+                std::memcpy(&hc, wk->pin, 16);
                 const int64_t counted = (int64_t)(hc.count - (unsigned long long)slot_base);
                 if (hc.empty || counted <= cap || attempt > 0) break;
                 SATMI_TRY(cand.reserve(8 * (size_t)counted * K));   // overflowed: re-run at the counted size
@@ -623,8 +628,9 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
             SATMI_TRY(exclusive_scan(flag.as<int64_t>(), pos.as<int64_t>(), nc, tiles.as<int64_t>(),
                                      grand.as<int64_t>(), s));
             int64_t nwin = 0;
-            SATMI_HIP(hipMemcpyAsync(&nwin, grand.p, 8, hipMemcpyDeviceToHost, s));
+            SATMI_HIP(hipMemcpyAsync(wk->pin + 2, grand.p, 8, hipMemcpyDeviceToHost, s));
             SATMI_HIP(hipStreamSynchronize(s));
+            nwin = (int64_t)wk->pin[2];
             if (nwin == 0) continue;
             SATMI_TRY(grow_clauses(ncl + nnew + nwin));
             hipLaunchKernelGGL(res_append_kernel, dim3(grid_for(nc)), dim3(PRIM_BLOCK), 0, s, cand.as<uint64_t>(),
