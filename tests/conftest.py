@@ -17,3 +17,20 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")
+
+
+def clause_set_sha(clauses):
+    """sha256 of a clause SET in make_golden_bench.py's canonical form (each
+    clause sorted, the clauses sorted, compact JSON)."""
+    import hashlib
+    import json
+    s = json.dumps(sorted(sorted(c) for c in clauses), separators=(",", ":"))
+    return hashlib.sha256(s.encode()).hexdigest()
+
+
+def clause_list_sha(clauses):
+    """sha256 of an ORDERED clause list (clause and literal order kept)."""
+    import hashlib
+    import json
+    s = json.dumps([list(c) for c in clauses], separators=(",", ":"))
+    return hashlib.sha256(s.encode()).hexdigest()

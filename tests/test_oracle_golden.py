@@ -6,6 +6,7 @@ import os
 import pytest
 
 import oracle
+from conftest import clause_list_sha, clause_set_sha
 
 
 def _load(golden_dir, name):
@@ -44,6 +45,43 @@ def test_resolution_matches_reference_passes(golden_dir):
         r = oracle.resolution(c["formula"], record=True)
         assert r["result"] == int(c["result"])
         assert r["clauses"] == c["passes"]
+
+
+def test_dp_php65_matches_reference_every_step(golden_dir):
+    """The configs[3] `php-dp` bench formula at full size: the oracle against
+    the reference's own davis_putnam_solver on PHP(6,5)
+    (tests/golden/dp_php65.json, make_golden_bench.py) -- the 30 eliminated
+    variables, the verdict, and every one of the 29 intermediate clause lists
+    (each clause in its set iteration order) by length and sha256, the first
+    four in full."""
+    (c,) = _load(golden_dir, "dp_php65.json")
+    r = oracle.dp(c["formula"], record=True, rec_cap=1 << 22)
+    assert r["result"] == int(c["result"]) == 0
+    assert r["vars"] == [s["var"] for s in c["steps"]] and len(r["vars"]) == 30
+    done = [s for s in c["steps"] if "sha256" in s]
+    assert len(done) == 29 and len(r["clauses"]) == 29
+    for k, s in enumerate(done):
+        assert len(r["clauses"][k]) == s["n"], k
+        assert sum(len(x) for x in r["clauses"][k]) == s["lits"], k
+        assert clause_list_sha(r["clauses"][k]) == s["sha256"], k
+        if "clauses" in s:
+            assert r["clauses"][k] == s["clauses"], k
+
+
+def test_resolution_php43_matches_reference_four_passes(golden_dir):
+    """The configs[3] `php-res` bench workload at full size: the oracle's
+    new-clause SET of each of the first four saturation passes of PHP(4,3)
+    equals the reference's own resolution_solver's (tests/golden/
+    resolution_php43.json, make_golden_bench.py): passes 1-3 clause by clause,
+    pass 4 (163,954 clauses) by size and sha256 of the canonical set."""
+    (c,) = _load(golden_dir, "resolution_php43.json")
+    r = oracle.resolution(c["formula"], record=True, max_passes=4, rec_cap=1 << 23)
+    assert r["result"] == -1 and r["passes"] == 4
+    assert r["pass_new"] == [p["count"] for p in c["passes"]] == [36, 270, 7132, 163954]
+    for k, p in enumerate(c["passes"]):
+        assert clause_set_sha(r["clauses"][k]) == p["sha256"], k
+        if "clauses" in p:
+            assert sorted(sorted(x) for x in r["clauses"][k]) == p["clauses"], k
 
 
 def test_sound_mode_verdicts_match_reference_dp(golden_dir):
