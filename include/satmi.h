@@ -117,6 +117,8 @@ int satmi_dpll_batch_host(int num_instances, const int32_t *h_inst_clause_begin,
  * clause set (CSR host arrays: clause c = lits[clause_off[c] .. clause_off[c+1])).
  * Clauses are variable bitsets in HBM; each pass resolves all pairs on the GPU
  * (tautologies filtered), dedups through a hash table over every clause key.
+ * Thread-safe: a call takes a device workspace (buffers + its own HIP stream)
+ * from a process-wide pool and returns it, so calls from several threads overlap.
  *   max_passes / clause_limit / time_limit_s   <= 0: unlimited
  *   *result   1 = True (no new clause derivable), 0 = False (empty resolvent),
  *             -1 = a limit stopped the saturation
@@ -136,9 +138,15 @@ int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, const int32
  * launches (HIP events on its stream), for rooflines. */
 int satmi_resolution_last_stats(int64_t *pairs, int64_t *candidates, double *pair_ms, double *claim_ms);
 
-/* Test knob: the pair kernel's first candidate append slot (default 0), so a
- * small pass exercises the slot arithmetic past 2^31 / 2^32 candidates. */
+/* Test knob: the first append slot (default 0) of the pair kernel's candidates
+ * (more than 31 variables) or of a pass's new clauses (at most 31), so a small
+ * pass exercises the slot arithmetic past 2^31 / 2^32. */
 int satmi_resolution_debug_slot_base(int64_t base);
+
+/* Test knob: cap of the candidate buffer of the > 31-variable path in bytes
+ * (0 = the default 1 GiB), so a small pass takes the re-run-at-the-counted-size
+ * path. */
+int satmi_resolution_debug_cand_bytes(int64_t bytes);
 
 /*
  * Davis-Putnam elimination, replaces davis_putnam_solver (REF.py:98-130) for one
@@ -152,8 +160,9 @@ int satmi_resolution_debug_slot_base(int64_t base);
  *   s is rec_step_off[s-1] .. rec_step_off[s] in rec_clause_off / rec_lits,
  *   every clause in its Python set iteration order; rec_step_off[s] is left
  *   untouched for a step that ended the elimination.
- * Thread-safe: each host thread runs its calls on its own HIP stream and
- * device buffers (kept between calls), so solves from several threads overlap.
+ * Thread-safe: a call takes a device workspace (buffers kept between calls,
+ * its own HIP stream) from a process-wide pool and returns it, so solves from
+ * several threads overlap and memory is bounded by the peak concurrency.
  */
 int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_lits, int64_t step_limit,
                   int64_t clause_limit, double time_limit_s, int32_t *h_result, int32_t *h_trace_vars,
@@ -166,6 +175,11 @@ int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_li
  * device time (HIP events on its stream), for rooflines. */
 int satmi_dp_last_stats(int64_t *steps, int64_t *subset_tests, int64_t *new_clauses, int64_t *candidate_bytes,
                         int *words, double *subsume_ms);
+
+/* Free the idle device workspaces that satmi_dp_host / satmi_resolution_host
+ * keep between calls (buffers only grow while kept); calls in flight keep theirs. */
+int satmi_dp_trim(void);
+int satmi_resolution_trim(void);
 
 /*
  * CDCL, replaces CDCLSolver / cdcl_solve (REF.py:217-384) for a batch of

@@ -6,25 +6,45 @@
 // empty resolvent, keep a resolvent unless an earlier-listed clause of
 // `remaining + unique_new` is a subset of it, continue with remaining + kept.
 //
-// GPU formulation, per step (host C++ drives the launches, data stays in HBM):
-//   * every clause carries (a) a bitset key over the dense variable index for
-//     the set algebra (split, tautology, emptiness, subsumption) and (b) its
-//     CPython table image (pyset_dev.h), because the reference's elimination
-//     order is decided by CPython's set layout;
-//   * dp_firstpos: first-occurrence position of every variable in the order
-//     `{abs(lit) for clause in clauses for lit in clause}` visits them (list
-//     order, then each clause's table order); dp_pop: one workgroup ranks the
-//     variables by that position and replays the comprehension's insertions
-//     into a modelled set, then pops its first live slot;
-//   * dp_split + scans: order-preserving compaction into pos / neg / rem lists;
-//   * dp_diff: `pc - {var}` / `nc - {-var}` images, one thread per clause;
-//   * dp_pairs: one thread per pair, resolvent bitset, tautology / empty flags;
-//   * dp_subsume: greedy `unique_new` filter.  A new clause is dropped iff a
-//     remaining clause or an *earlier* new clause is a subset of it (an earlier
-//     new clause that was itself dropped was dropped for a subset that is also
-//     a subset of this one), so the greedy loop becomes one parallel test;
-//   * dp_build: `AX | BY` images of the kept resolvents; dp_assemble: the next
-//     clause list (rem in order, then kept in pair order).
+// GPU formulation.  Every clause carries (a) a bitset key over the dense
+// variable index for the set algebra and (b) its CPython table image
+// (pyset_dev.h) in an image arena, because the reference's elimination order
+// is decided by CPython's set layout.  A step is a fixed sequence of eight
+// launches whose sizes live on the device (DpState): the host enqueues whole
+// batches of steps and waits once per batch -- a step never waits on the host.
+//
+//   pop_split  (1 workgroup) variables.pop() from the first-position table the
+//              previous step left, then the order-preserving split into the
+//              pos / neg / rem lists (block prefix sums);
+//   pairs      resolvent key of every (pos, neg) pair, tautology / empty
+//              flags, the non-tautological pairs as a bitmap;
+//   hash       one representative per distinct resolvent: the FIRST pair (in
+//              pair order) holding that key, by atomicMin in a hash table;
+//   remtest    every representative against the remaining clauses (2-D grid:
+//              representative tiles x rem chunks, rem keys broadcast from LDS);
+//   survlist   the representatives no rem clause subsumes (and the table
+//              cleared for the next step);
+//   survtest   every survivor against the survivors earlier in pair order;
+//   kept       (1 workgroup) the empty-clause / clause-limit verdict, the kept
+//              survivors in pair order (bitmap + block scan), capacities;
+//   assemble   the next clause list: rem clauses (their images stay where they
+//              are) + the kept resolvents' images `(pc - {var}) | (nc - {-var})`
+//              built in the arena, and the next step's first-position table.
+//
+// Why this equals the reference's greedy `unique_new` (REF.py:122-125): a new
+// clause x is dropped iff a rem clause or an earlier KEPT new clause is a
+// subset of it.  That equals "a rem clause or ANY earlier new clause is a
+// subset": an earlier new clause y that was itself dropped was dropped for a
+// subset z (rem or kept before y) that is also a subset of x.  The earlier
+// new clauses can further be narrowed to earlier representatives that
+// survived the rem test: a duplicate of an earlier clause has that earlier
+// representative, and a y with a rem subset r gives x the same r.  So x is
+// kept iff x is its key's first occurrence, no rem clause is a subset of x,
+// and no earlier rem-surviving representative is a subset of x.
+//
+// Capacities are host-known; a step whose sizes exceed one sets `overflow`
+// (nothing of the step's input is lost), the host grows the buffer and
+// resumes from that step.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -40,29 +60,148 @@ namespace satmi {
 
 // smallest power of two >= 8 that exceeds 8*u: room for every table a set of u
 // keys passes through (add: < 8u, merge: < 4u)
-static inline int64_t cap_for(int64_t u) {
+__host__ __device__ static inline int64_t cap_for(int64_t u) {
     int64_t c = PY_MINSIZE;
     while (c <= 8 * u) c <<= 1;
     return c;
 }
 
-struct ClauseList {   // device arrays of one generation
-    int64_t *off;      // table image offset in pool
-    int32_t *mask, *fill, *used;
-    uint64_t *bits;    // K words per clause
-    int32_t *pool;
+// overflow bits (DpState::overflow) and what the host grows for each
+enum : int32_t { OVF_PAIRS = 1, OVF_NCL = 2, OVF_ARENA = 4, OVF_XS = 8 };
+
+constexpr uint64_t DP_EMPTY = ~0ull;
+
+// The solve's state, on the device.  Host writes it once per solve (and on a
+// resume); kernels read sizes from it and one thread of the single-workgroup
+// kernels updates it.
+struct DpState {
+    int64_t ncl, ncl2;             // clauses of g[cur]; of the generation being assembled (pending)
+    int64_t np, nn, nr, npairs;    // this step's split
+    int64_t nontaut, nuniq, nsurv, nkept;
+    int64_t arena_top, arena_base;   // image arena bump pointer; this step's kept images
+    int64_t tests, new_total;        // subset tests, non-tautological resolvents (whole solve)
+    int64_t need[4];                 // sizes wanted on overflow (pairs, ncl, arena, xs)
+    uint64_t first_empty;            // first pair (in pair order) with an empty resolvent
+    uint64_t t0;                     // s_memrealtime at the solve's start
+    int32_t cur, pending, done, result, steps, overflow, set_ovf, var, d;
+    int32_t mxA, mxB, capA, capB, capR, epoch, pad;
 };
 
-__device__ __forceinline__ DView cl_view(const ClauseList &L, int64_t c) {
-    return {L.pool + L.off[c], (int64_t)L.mask[c], (int64_t)L.fill[c], (int64_t)L.used[c]};
+struct ClauseList {   // one generation of the clause list
+    int64_t *off;     // image offset in the arena
+    int32_t *mask, *fill, *used;
+    uint64_t *bits;   // K words per clause: positive then negative literal bits
+};
+
+// Everything a step's kernels touch, by value (pointers + host-known capacities).
+struct DpArgs {
+    DpState *st;
+    ClauseList g[2];
+    int32_t *arena;
+    int64_t arena_cap;
+    const int32_t *v2d, *d2v;
+    int V, W, K;
+    unsigned long long *firstpos;   // per dense variable: (clause << 32 | slot) of its first visit
+    int32_t *order, *popscratch;
+    int64_t popcap;
+    int64_t *plist, *nlist, *rlist;
+    int64_t ncl_cap;
+    uint64_t *rbits, *ntbits;       // resolvent keys; non-tautological pairs bitmap (64 per word)
+    int64_t pair_cap;               // < 2^31: pair indices are 32-bit
+    uint64_t *table;                // hash table of representatives (pair index, DP_EMPTY)
+    uint64_t tmask;
+    uint32_t *uslot;                // table slot of each distinct key
+    int32_t *dropped, *hit;         // epoch stamps: representative subsumed by rem / survivor hit
+    uint32_t *surv, *klist;         // survivors' pair indices; kept pairs in pair order
+    uint64_t *rkeys, *ukeys, *skeys;  // contiguous keys: rem clauses, representatives, survivors
+    uint32_t *keptbits;             // kept pairs (32 per word), cleared as compacted
+    int32_t *xs;                    // per kept resolvent: AX and BY image scratch
+    int64_t xs_cap;
+    int32_t *trace;
+    int trace_cap;
+    int64_t step_limit, clause_limit;
+    uint64_t limit_ticks;
+};
+
+__device__ __forceinline__ DView cl_view(const ClauseList &L, const int32_t *arena, int64_t c) {
+    return {arena + L.off[c], (int64_t)L.mask[c], (int64_t)L.fill[c], (int64_t)L.used[c]};
 }
 
-// clauses = [set(clause) for clause in formula]  (REF.py:99); image c at pool + 2*cap*c
-__global__ void dp_encode_kernel(int nclauses, const int32_t *off, const int32_t *lits, const int32_t *var2dense,
-                                 int W, int64_t cap, ClauseList L, int *overflow) {
-    const int K = 2 * W;
+// block-wide exclusive prefix sum (every thread of the block calls it)
+__device__ __forceinline__ int block_excl_scan(int x, int *wsum, int &total) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int incl = wave_incl_scan(x);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        const int v = wsum[w];
+        off += w < wid ? v : 0;
+        tot += v;
+    }
+    __syncthreads();
+    total = tot;
+    return off + incl - x;
+}
+
+__device__ __forceinline__ int block_sum(int x, int *wsum) {
+    int t;
+    (void)block_excl_scan(x, wsum, t);
+    return t;
+}
+
+__device__ __forceinline__ int block_max(int x, int *wsum) {
+    const int m = wave_max_i32(x);
+    const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane_id() == 0) wsum[wid] = m;
+    __syncthreads();
+    int r = 0;
+    for (int w = 0; w < nw; ++w) r = max(r, wsum[w]);
+    __syncthreads();
+    return r;
+}
+
+// The visiting order of `{abs(lit) for clause in clauses for lit in clause}`
+// (REF.py:100/:128): clause t's table slot i is position (t << 32 | i).  The
+// first position of every variable is an atomicMin, reduced in LDS per block
+// when the variables fit.
+constexpr int FP_LDS = 2048;
+__device__ __forceinline__ void firstpos_clause(const DpArgs &A, unsigned long long *lfp, const int32_t *t, int64_t mask,
+                                                int64_t c) {
+    for (int64_t i = 0; i <= mask; ++i) {
+        const int32_t k = t[i];
+        if (k == PY_EMPTY || k == PY_DUMMY) continue;
+        const int d = A.v2d[k < 0 ? -k : k];
+        const unsigned long long pos = ((unsigned long long)c << 32) | (unsigned long long)i;
+        if (lfp)
+            atomicMin(&lfp[d], pos);
+        else
+            atomicMin(&A.firstpos[d], pos);
+    }
+}
+__device__ __forceinline__ void firstpos_begin(const DpArgs &A, unsigned long long *lfp) {
+    if (A.V <= FP_LDS)
+        for (int d = threadIdx.x; d < A.V; d += blockDim.x) lfp[d] = ~0ull;
+    __syncthreads();
+}
+__device__ __forceinline__ void firstpos_flush(const DpArgs &A, unsigned long long *lfp) {
+    __syncthreads();
+    if (A.V <= FP_LDS)
+        for (int d = threadIdx.x; d < A.V; d += blockDim.x)
+            if (lfp[d] != ~0ull) atomicMin(&A.firstpos[d], lfp[d]);
+}
+
+// clauses = [set(clause) for clause in formula]  (REF.py:99): image c at arena + 2*cap*c
+__global__ void __launch_bounds__(256) dp_encode_kernel(DpArgs A, int nclauses, const int32_t *off,
+                                                        const int32_t *lits, int64_t cap) {
+    __shared__ unsigned long long lfp_sh[FP_LDS];
+    unsigned long long *lfp = A.V <= FP_LDS ? lfp_sh : nullptr;
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.st->t0 = __builtin_amdgcn_s_memrealtime();
+    firstpos_begin(A, lfp);
+    const ClauseList L = A.g[0];
+    const int W = A.W, K = A.K;
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nclauses; c += gridDim.x * blockDim.x) {
-        int32_t *a = L.pool + (int64_t)c * 2 * cap;
+        int32_t *a = A.arena + (int64_t)c * 2 * cap;
         DSet s;
         dset_init(s, a, a + cap, cap);
         uint64_t *k = L.bits + (int64_t)c * K;
@@ -70,329 +209,626 @@ __global__ void dp_encode_kernel(int nclauses, const int32_t *off, const int32_t
         for (int j = off[c]; j < off[c + 1]; ++j) {
             const int x = lits[j];
             py_add(s, x);
-            const int d = var2dense[x < 0 ? -x : x];
+            const int d = A.v2d[x < 0 ? -x : x];
             k[(x < 0 ? W : 0) + (d >> 6)] |= 1ull << (d & 63);
         }
-        if (s.overflow) *overflow = 1;
-        L.off[c] = s.t - L.pool;
+        if (s.overflow) A.st->set_ovf = 1;
+        L.off[c] = s.t - A.arena;
         L.mask[c] = (int32_t)s.mask;
         L.fill[c] = (int32_t)s.fill;
         L.used[c] = (int32_t)s.used;
+        firstpos_clause(A, lfp, s.t, s.mask, c);
     }
+    firstpos_flush(A, lfp);
 }
 
-__global__ void dp_used_kernel(ClauseList L, int64_t n, int64_t *used) {
+// the first-position table of g[cur] from scratch (a resumed solve)
+__global__ void __launch_bounds__(256) dp_firstpos_kernel(DpArgs A) {
+    __shared__ unsigned long long lfp_sh[FP_LDS];
+    unsigned long long *lfp = A.V <= FP_LDS ? lfp_sh : nullptr;
+    firstpos_begin(A, lfp);
+    const DpState *S = A.st;
+    const ClauseList L = A.g[S->cur];
+    const int64_t n = S->ncl;
     for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
-        used[c] = L.used[c];
+        firstpos_clause(A, lfp, A.arena + L.off[c], L.mask[c], c);
+    firstpos_flush(A, lfp);
 }
 
-// first position of every variable in the comprehension's visiting order
-__global__ void dp_firstpos_kernel(ClauseList L, int64_t n, const int64_t *base, const int32_t *var2dense,
-                                   unsigned long long *firstpos) {
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
-        const DView s = cl_view(L, c);
-        int64_t p = base[c];
-        for (int64_t i = 0; i <= s.mask; ++i) {
-            const int32_t k = s.t[i];
-            if (k == PY_EMPTY || k == PY_DUMMY) continue;
-            atomicMin(&firstpos[var2dense[k < 0 ? -k : k]], (unsigned long long)p);
-            ++p;
+// variables.pop() (REF.py:100-103, :128) and the split (REF.py:106-108): one
+// workgroup of 1024 threads.
+constexpr int POP_THREADS = 1024;
+constexpr int POP_LDS = 2048;   // model-set table slots kept in LDS (cap_for(V) <= this: V <= 255)
+__global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
+    __shared__ unsigned long long fp_sh[FP_LDS];
+    __shared__ int32_t ord_sh[FP_LDS];
+    __shared__ int32_t pop_sh[2 * POP_LDS];
+    __shared__ int wsum[16];
+    __shared__ int64_t sh_ncl;
+    __shared__ int sh_cur, sh_quit, sh_var;
+    DpState *S = A.st;
+    if (S->done) return;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        if (S->pending) {   // the previous step's generation becomes the clause list
+            S->cur ^= 1;
+            S->ncl = S->ncl2;
+            S->pending = 0;
         }
+        sh_cur = S->cur;
+        sh_ncl = S->ncl;
+        sh_quit = 0;
     }
+    const int V = A.V;
+    const bool lds_fp = V <= FP_LDS;
+    if (lds_fp)
+        for (int d = tid; d < V; d += POP_THREADS) fp_sh[d] = A.firstpos[d];
+    __syncthreads();
+    // rank the variables by first position (positions are distinct)
+    int live = 0;
+    for (int d = tid; d < V; d += POP_THREADS) {
+        const unsigned long long f = lds_fp ? fp_sh[d] : A.firstpos[d];
+        if (f == ~0ull) continue;
+        ++live;
+        int rank = 0;
+        for (int e = 0; e < V; ++e) rank += (lds_fp ? fp_sh[e] : A.firstpos[e]) < f ? 1 : 0;
+        (lds_fp ? ord_sh : A.order)[rank] = A.d2v[d];
+    }
+    const int nv = block_sum(live, wsum);
+    if (tid == 0) {
+        int32_t popped = 0;
+        if (nv == 0) {   // `while variables` ends: True (REF.py:130)
+            S->result = 1;
+            S->done = 1;
+            sh_quit = 1;
+        } else {
+            // the model set in LDS when it fits (a chain of dependent probes)
+            DSet s;
+            int32_t *ps = A.popcap <= POP_LDS ? pop_sh : A.popscratch;
+            dset_init(s, ps, ps + A.popcap, A.popcap);
+            const int32_t *ord = lds_fp ? ord_sh : A.order;
+            for (int r = 0; r < nv; ++r) py_add(s, ord[r]);
+            if (s.overflow) {
+                S->set_ovf = 1;
+                S->done = 1;
+                sh_quit = 1;
+            } else {
+                for (int64_t i = 0; i <= s.mask; ++i)   // a fresh set's finger is 0: first live slot
+                    if (s.t[i] != PY_EMPTY && s.t[i] != PY_DUMMY) {
+                        popped = s.t[i];
+                        break;
+                    }
+            }
+            if (!sh_quit && A.step_limit > 0 && S->steps >= A.step_limit) {
+                S->result = -1;
+                S->done = 1;
+                sh_quit = 1;
+            }
+            if (!sh_quit && A.limit_ticks && __builtin_amdgcn_s_memrealtime() - S->t0 > A.limit_ticks) {
+                S->result = -1;
+                S->done = 1;
+                sh_quit = 1;
+            }
+        }
+        sh_var = popped;
+    }
+    __syncthreads();
+    if (sh_quit) return;
+    const int32_t var = sh_var;
+    const int d = A.v2d[var];
+    const int W = A.W, K = A.K, dw = d >> 6, db = d & 63;
+    const ClauseList L = A.g[sh_cur];
+    const int64_t ncl = sh_ncl;
+    int64_t np = 0, nn = 0, nr = 0;
+    int mxA = 0, mxB = 0;
+    for (int64_t b0 = 0; b0 < ncl; b0 += POP_THREADS) {
+        const int64_t c = b0 + tid;
+        const bool valid = c < ncl;
+        bool p = false, q = false;
+        if (valid) {
+            p = (L.bits[c * K + dw] >> db) & 1ull;
+            q = (L.bits[c * K + W + dw] >> db) & 1ull;
+            const int u = L.used[c];
+            if (p) mxA = max(mxA, u);
+            if (q) mxB = max(mxB, u);
+        }
+        int tot, tr;
+        const int ex = block_excl_scan((p ? 1 : 0) | (q ? 1 << 16 : 0), wsum, tot);
+        const int er = block_excl_scan(valid && !p && !q ? 1 : 0, wsum, tr);   // a clause may be in both lists
+        const int ep = ex & 0xFFFF, en = ex >> 16;
+        if (p) A.plist[np + ep] = c;
+        if (q) A.nlist[nn + en] = c;
+        if (valid && !p && !q) {
+            A.rlist[nr + er] = c;
+            for (int w = 0; w < K; ++w) A.rkeys[(nr + er) * K + w] = L.bits[c * K + w];
+        }
+        np += tot & 0xFFFF;
+        nn += tot >> 16;
+        nr += tr;
+    }
+    mxA = block_max(mxA, wsum);
+    mxB = block_max(mxB, wsum);
+    const int64_t npairs = np * nn;
+    if (npairs > A.pair_cap) {   // grow the pair buffers and run this step again
+        if (tid == 0) {
+            S->need[0] = npairs;
+            S->overflow |= OVF_PAIRS;
+            S->done = 1;
+        }
+        return;
+    }
+    if (tid == 0) {
+        if (S->steps < A.trace_cap) A.trace[S->steps] = var;
+        S->steps += 1;
+        S->var = var;
+        S->d = d;
+        S->np = np;
+        S->nn = nn;
+        S->nr = nr;
+        S->npairs = npairs;
+        S->mxA = mxA;
+        S->mxB = mxB;
+        S->capA = (int32_t)cap_for(mxA);
+        S->capB = (int32_t)cap_for(mxB);
+        S->capR = (int32_t)cap_for((int64_t)mxA + mxB);
+        S->first_empty = DP_EMPTY;
+        S->nontaut = 0;
+        S->nuniq = 0;
+        S->nsurv = 0;
+        S->nkept = 0;
+        S->epoch += 1;
+    }
+    for (int e = tid; e < V; e += POP_THREADS) A.firstpos[e] = ~0ull;   // for the next step's assembly
 }
 
-// variables.pop() (REF.py:100-103, :128): one workgroup.  out[0] = popped
-// variable (0: the set is empty), out[1] = number of distinct variables.
-__global__ void __launch_bounds__(256) dp_pop_kernel(const unsigned long long *firstpos, const int32_t *dense2var,
-                                                     int V, int32_t *order, int32_t *scratch, int64_t cap,
-                                                     int32_t *out) {
-    __shared__ int nlive;
-    if (threadIdx.x == 0) nlive = 0;
-    __syncthreads();
-    for (int d = threadIdx.x; d < V; d += blockDim.x) {
-        const unsigned long long f = firstpos[d];
-        if (f == ~0ull) continue;
-        int rank = 0;
-        for (int e = 0; e < V; ++e) rank += firstpos[e] < f ? 1 : 0;   // positions are distinct
-        order[rank] = dense2var[d];
-        atomicAdd(&nlive, 1);
+// pair p = i*nn + j: resolvent key, tautology (REF.py:115) and empty (REF.py:117)
+// flags; rbits[p] for non-tautological pairs, ntbits bit p.
+__global__ void __launch_bounds__(256) dp_pairs_kernel(DpArgs A) {
+    __shared__ int wsum[4];
+    DpState *S = A.st;
+    if (S->done) return;
+    const uint32_t npairs = (uint32_t)S->npairs, nn = (uint32_t)S->nn;
+    const int d = S->d, W = A.W, K = A.K;
+    const ClauseList L = A.g[S->cur];
+    const uint64_t vb = 1ull << (d & 63);
+    const int vw = d >> 6, lane = lane_id();
+    int cnt = 0;
+    for (uint32_t p0 = blockIdx.x * 256u + (threadIdx.x & ~63u); p0 < npairs; p0 += gridDim.x * 256u) {
+        const uint32_t p = p0 + lane;
+        bool nt = false;
+        if (p < npairs) {
+            const uint32_t i = p / nn, j = p - i * nn;
+            const uint64_t *a = L.bits + A.plist[i] * K, *b = L.bits + A.nlist[j] * K;
+            uint64_t *r = A.rbits + (uint64_t)p * K;
+            bool taut = false, empty = true;
+            for (int w = 0; w < W; ++w) {
+                // (pc - {var}) | (nc - {-var}): var leaves pc's positive half and
+                // -var nc's negative half only (a tautological pc keeps its -var)
+                const uint64_t keep = w == vw ? ~vb : ~0ull;
+                const uint64_t rp = (a[w] & keep) | b[w], rn = a[W + w] | (b[W + w] & keep);
+                r[w] = rp;
+                r[W + w] = rn;
+                taut |= (rp & rn) != 0ull;
+                empty &= (rp | rn) == 0ull;
+            }
+            if (empty) atomicMin((unsigned long long *)&S->first_empty, (unsigned long long)p);
+            nt = !taut && !empty;
+        }
+        const uint64_t m = __ballot(nt);
+        if (lane == 0) A.ntbits[p0 >> 6] = m;
+        cnt += lane == 0 ? __popcll(m) : 0;
     }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    const int nv = nlive;
-    int32_t popped = 0;
-    if (nv > 0) {
-        DSet s;
-        dset_init(s, scratch, scratch + cap, cap);
-        for (int r = 0; r < nv; ++r) py_add(s, order[r]);
-        if (s.overflow) {
-            out[2] = 1;
-        } else {
-            for (int64_t i = 0; i <= s.mask; ++i)   // a fresh set's finger is 0: first live slot
-                if (s.t[i] != PY_EMPTY && s.t[i] != PY_DUMMY) {
-                    popped = s.t[i];
+    const int tot = block_sum(cnt, wsum);
+    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long *)&S->nontaut, (unsigned long long)tot);
+}
+
+__device__ __forceinline__ uint64_t dp_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// one representative per distinct resolvent key: the table slot holds the
+// smallest pair index with that key (atomicMin); the slot of each key's first
+// claim goes to uslot.
+__global__ void __launch_bounds__(256) dp_hash_kernel(DpArgs A) {
+    DpState *S = A.st;
+    if (S->done || S->first_empty != DP_EMPTY) return;   // the step ends in an empty clause
+    const uint32_t npairs = (uint32_t)S->npairs;
+    const int K = A.K, lane = lane_id();
+    for (uint32_t p0 = blockIdx.x * 256u + (threadIdx.x & ~63u); p0 < npairs; p0 += gridDim.x * 256u) {
+        const uint32_t p = p0 + lane;
+        const bool nt = p < npairs && ((A.ntbits[p0 >> 6] >> lane) & 1ull);
+        bool claimed = false;
+        uint64_t slot = 0;
+        if (nt) {
+            const uint64_t *x = A.rbits + (uint64_t)p * K;
+            uint64_t h = 0x9E3779B97F4A7C15ull;
+            for (int w = 0; w < K; ++w) h = dp_mix64(h ^ x[w]) + (uint64_t)w;
+            uint64_t s = h & A.tmask;
+            for (;;) {
+                uint64_t cur = __hip_atomic_load(A.table + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cur == DP_EMPTY) {
+                    cur = atomicCAS((unsigned long long *)(A.table + s), (unsigned long long)DP_EMPTY,
+                                    (unsigned long long)p);
+                    if (cur == DP_EMPTY) {
+                        claimed = true;
+                        slot = s;
+                        break;
+                    }
+                }
+                const uint64_t *y = A.rbits + cur * K;
+                bool eq = true;
+                for (int w = 0; w < K; ++w) eq &= y[w] == x[w];
+                if (eq) {
+                    if (p < cur) atomicMin((unsigned long long *)(A.table + s), (unsigned long long)p);
                     break;
                 }
+                s = (s + 1) & A.tmask;
+            }
+        }
+        const uint64_t bal = __ballot(claimed);
+        if (bal) {
+            uint32_t base = 0;
+            if (lane == 0) base = (uint32_t)atomicAdd((unsigned long long *)&S->nuniq, (unsigned long long)__popcll(bal));
+            base = uniform_u32(base);
+            if (claimed) A.uslot[base + __popcll(bal & lanemask_lt())] = (uint32_t)slot;
         }
     }
-    out[0] = popped;
-    out[1] = nv;
 }
 
-// split flags (REF.py:106-108)
-// Also the largest image (`used`) among the clauses holding var / -var into
-// mx[0] / mx[1] (zeroed by the host): the capacities of the step's images,
-// read back with the split counts instead of after the filter.
-__global__ void dp_split_kernel(ClauseList L, int64_t n, int W, int d, int64_t *fpos, int64_t *fneg, int64_t *frem,
-                                unsigned long long *mx) {
-    const int K = 2 * W;
-    int up = 0, un = 0;
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t *k = L.bits + c * K;
-        const bool p = (k[d >> 6] >> (d & 63)) & 1ull;
-        const bool q = (k[W + (d >> 6)] >> (d & 63)) & 1ull;
-        fpos[c] = p;
-        fneg[c] = q;
-        frem[c] = !p && !q;
-        const int u = (p || q) ? L.used[c] : 0;
-        up = p ? max(up, u) : up;
-        un = q ? max(un, u) : un;
-    }
-    up = wave_max_i32(up);   // every lane reaches here (grid-stride loop)
-    un = wave_max_i32(un);
-    if (lane_id() == 0) {
-        if (up) atomicMax(mx, (unsigned long long)up);
-        if (un) atomicMax(mx + 1, (unsigned long long)un);
-    }
-}
-
-__global__ void dp_compact_kernel(const int64_t *flag, const int64_t *pos, int64_t n, int64_t *out) {
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
-        if (flag[c]) out[pos[c]] = c;
-}
-
-struct Images {   // per-entry images built into 2*cap slots each
-    int32_t *pool;
-    int64_t *off;
-    int32_t *mask, *fill, *used;
-    int64_t cap;
+// Subset tests "y is a subset of x" with x (the tested clause) in registers
+// and the candidate keys y staged 256 at a time in LDS from a contiguous copy
+// (every lane reads the same address: a broadcast); four tests per step of
+// the candidate loop, so four LDS reads are in flight before the branch.  KT =
+// key words (2W) known at compile time, 0 = any width (keys read from memory).
+template <int KT>
+struct KeyReg {
+    uint64_t w[KT ? KT : 1];
 };
 
-__device__ __forceinline__ DView img_view(const Images &I, int64_t e) {
-    return {I.pool + I.off[e], (int64_t)I.mask[e], (int64_t)I.fill[e], (int64_t)I.used[e]};
+constexpr int TEST_TILE = 256;
+
+template <int KT>
+__device__ __forceinline__ bool subset_of(const uint64_t *y, const KeyReg<KT> &x, const uint64_t *xg, int K) {
+    uint64_t out = 0;
+    if constexpr (KT > 0) {
+#pragma unroll
+        for (int w = 0; w < KT; ++w) out |= y[w] & ~x.w[w];
+    } else {
+        for (int w = 0; w < K; ++w) out |= y[w] & ~xg[w];
+    }
+    return out == 0ull;
 }
 
-// AX = pc - {var} for the pos list, BY = nc - {-var} for the neg list
-__global__ void dp_diff_kernel(ClauseList L, const int64_t *list, int64_t n, int32_t key, Images I, int *overflow) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        int32_t *a = I.pool + e * 2 * I.cap;
-        DSet s;
-        dset_init(s, a, a + I.cap, I.cap);
-        py_difference1(s, cl_view(L, list[e]), key);
-        if (s.overflow) *overflow = 1;
-        I.off[e] = s.t - I.pool;
-        I.mask[e] = (int32_t)s.mask;
-        I.fill[e] = (int32_t)s.fill;
-        I.used[e] = (int32_t)s.used;
+// Items = (x tile of 256 tested clauses) x (y tile of 256 candidates); block b
+// takes items b, b + gridDim.x, ...  Lane l of an item tests x = tile x, lane
+// l against the candidates of tile y with cand_ok(j) (all rem clauses; the
+// survivors earlier in pair order), marking stamp[x] = epoch at the first
+// subset; a lane whose x another block already marked stops.
+template <int KT, bool SURV>
+__device__ __forceinline__ void dp_test_items(const DpArgs &A, int64_t nx, int64_t ny, const uint64_t *xkeys,
+                                              const uint64_t *ykeys, const uint32_t *ypair, int32_t *stamp,
+                                              int32_t epoch, int &tests) {
+    __shared__ uint64_t tile[TEST_TILE * (KT ? KT : 1)];
+    __shared__ uint32_t tp[TEST_TILE];
+    const int K = A.K, tid = threadIdx.x;
+    const int64_t ntx = (nx + TEST_TILE - 1) / TEST_TILE, nty = (ny + TEST_TILE - 1) / TEST_TILE;
+    for (int64_t item = blockIdx.x; item < ntx * nty; item += gridDim.x) {
+        const int64_t tx = item % ntx, ty = item / ntx;
+        const int64_t u = tx * TEST_TILE + tid;
+        const bool valid = u < nx;
+        const uint64_t *xg = xkeys + (valid ? u : 0) * K;
+        KeyReg<KT> x;
+        if constexpr (KT > 0) {
+#pragma unroll
+            for (int w = 0; w < KT; ++w) x.w[w] = valid ? xg[w] : ~0ull;
+        }
+        const uint32_t px = SURV && valid ? ypair[u] : 0u;
+        bool alive = valid && __hip_atomic_load(stamp + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch;
+        const int64_t e0 = ty * TEST_TILE;
+        const int cnt = (int)min<int64_t>(TEST_TILE, ny - e0);
+        if (__syncthreads_or(alive)) {
+            if (tid < cnt) {
+                if constexpr (KT > 0) {
+#pragma unroll
+                    for (int w = 0; w < KT; ++w) tile[tid * KT + w] = ykeys[(e0 + tid) * KT + w];
+                }
+                if (SURV) tp[tid] = ypair[e0 + tid];
+            }
+            __syncthreads();
+            if (alive) {
+                const auto yk = [&](int j) { return KT ? tile + j * (KT ? KT : 1) : ykeys + (e0 + j) * K; };
+                const auto ok = [&](int j) { return j < cnt && (!SURV || tp[j] < px); };
+                int j = 0;
+                for (; j < cnt; j += 4) {
+                    const bool s0 = ok(j) && subset_of<KT>(yk(j), x, xg, K);
+                    const bool s1 = ok(j + 1) && subset_of<KT>(yk(j + 1), x, xg, K);
+                    const bool s2 = ok(j + 2) && subset_of<KT>(yk(j + 2), x, xg, K);
+                    const bool s3 = ok(j + 3) && subset_of<KT>(yk(j + 3), x, xg, K);
+                    if (s0 | s1 | s2 | s3) {
+                        __hip_atomic_store(stamp + u, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        j += 4;
+                        break;
+                    }
+                }
+                tests += min(j, cnt);
+            }
+        }
+        __syncthreads();   // the tile is rewritten by the next item
     }
 }
 
-// pair p = i*nn + j: resolvent bitset, tautology (REF.py:115) and empty (REF.py:117) flags
-__global__ void dp_pairs_kernel(ClauseList L, const int64_t *plist, const int64_t *nlist, int64_t nn, int64_t npairs,
-                                int W, int d, uint64_t *rbits, int64_t *nontaut, unsigned long long *first_empty) {
-    const int K = 2 * W;
-    const uint64_t vb = 1ull << (d & 63);
-    const int vw = d >> 6;
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npairs;
-         p += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t *a = L.bits + plist[p / nn] * K, *b = L.bits + nlist[p % nn] * K;
-        uint64_t *r = rbits + p * K;
-        bool taut = false, empty = true;
-        for (int w = 0; w < W; ++w) {
-            // (pc - {var}) | (nc - {-var}): var leaves pc's positive half and
-            // -var nc's negative half only (a tautological pc keeps its -var)
-            const uint64_t keep = w == vw ? ~vb : ~0ull;
-            const uint64_t rp = (a[w] & keep) | b[w], rn = a[W + w] | (b[W + w] & keep);
-            r[w] = rp;
-            r[W + w] = rn;
-            taut |= (rp & rn) != 0ull;
-            empty &= (rp | rn) == 0ull;
-        }
-        nontaut[p] = !taut;
-        if (empty) atomicMin(first_empty, (unsigned long long)p);
+// every representative against the remaining clauses (REF.py:124, remaining
+// part); the representatives' keys are gathered first (x side, contiguous)
+template <int KT>
+__global__ void __launch_bounds__(TEST_TILE) dp_remtest_kernel(DpArgs A) {
+    __shared__ int wsum[4];
+    DpState *S = A.st;
+    if (S->done || S->first_empty != DP_EMPTY) return;
+    int tests = 0;
+    dp_test_items<KT, false>(A, S->nuniq, S->nr, A.ukeys, A.rkeys, nullptr, A.dropped, S->epoch, tests);
+    const int tot = block_sum(tests, wsum);
+    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long *)&S->tests, (unsigned long long)tot);
+}
+
+// the keys of the distinct representatives, contiguous (remtest's x side)
+__global__ void __launch_bounds__(256) dp_gather_kernel(DpArgs A) {
+    DpState *S = A.st;
+    if (S->done || S->first_empty != DP_EMPTY) return;
+    const int64_t nuniq = S->nuniq;
+    const int K = A.K;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nuniq * K; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = e / K;
+        const uint64_t p = A.table[A.uslot[u]];
+        A.ukeys[e] = A.rbits[p * K + (e - u * K)];
     }
 }
 
-__device__ __forceinline__ bool bits_subset(const uint64_t *a, const uint64_t *b, int K) {
-    for (int w = 0; w < K; ++w)
-        if (a[w] & ~b[w]) return false;
-    return true;
-}
-
-// unique_new (REF.py:122-125): kept[k] iff no rem clause and no earlier new
-// clause is a subset.  One wavefront per new clause: its 64 lanes test 64
-// candidate subsets per step and the wave stops at the first hit (ballot), so
-// the O(m (nrem + m)) tests spread over every wave slot of the chip instead of
-// one serial loop per thread.
-__global__ void __launch_bounds__(256) dp_subsume_kernel(ClauseList L, const int64_t *rlist, int64_t nrem,
-                                                         const uint64_t *rbits, const int64_t *ntlist, int64_t m,
-                                                         int K, int64_t *kept) {
-    const int ln = lane_id();
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; k < m; k += nwaves) {
-        const uint64_t *x = rbits + ntlist[k] * K;
-        bool sub = false;
-        for (int64_t e0 = 0; e0 < nrem && !sub; e0 += 64) {
-            const int64_t e = e0 + ln;
-            sub = __ballot(e < nrem && bits_subset(L.bits + rlist[e] * K, x, K)) != 0ull;
+// the representatives no rem clause subsumes (pair index + key, contiguous);
+// every used table slot cleared for the next step
+__global__ void __launch_bounds__(256) dp_survlist_kernel(DpArgs A) {
+    DpState *S = A.st;
+    if (S->done || S->first_empty != DP_EMPTY) return;
+    const int64_t nuniq = S->nuniq;
+    const int32_t epoch = S->epoch;
+    const int lane = lane_id(), K = A.K;
+    for (int64_t u0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); u0 < nuniq; u0 += (int64_t)gridDim.x * 256) {
+        const int64_t u = u0 + lane;
+        bool keep = false;
+        uint32_t p = 0;
+        if (u < nuniq) {
+            const uint32_t s = A.uslot[u];
+            p = (uint32_t)A.table[s];
+            A.table[s] = DP_EMPTY;
+            keep = A.dropped[u] != epoch;
         }
-        for (int64_t e0 = 0; e0 < k && !sub; e0 += 64) {
-            const int64_t e = e0 + ln;
-            sub = __ballot(e < k && bits_subset(rbits + ntlist[e] * K, x, K)) != 0ull;
+        const uint64_t bal = __ballot(keep);
+        if (bal) {
+            uint32_t base = 0;
+            if (lane == 0) base = (uint32_t)atomicAdd((unsigned long long *)&S->nsurv, (unsigned long long)__popcll(bal));
+            base = uniform_u32(base);
+            if (keep) {
+                const uint32_t at = base + __popcll(bal & lanemask_lt());
+                A.surv[at] = p;
+                for (int w = 0; w < K; ++w) A.skeys[(uint64_t)at * K + w] = A.ukeys[u * K + w];
+            }
         }
-        if (ln == 0) kept[k] = !sub;
     }
 }
 
-// The same filter for K <= 8 words per clause (<= 256 variables), one LANE per
-// new clause with its key in registers.  Candidates are numbered c = 0 ..
-// nrem + m: remaining clauses first, then new clauses (new clause e is a
-// candidate of k only when e < k).  Block (x, y) tests the new clauses
-// sel[256x .. 256x + 256) (sel == nullptr: k = 256x + lane) against candidates
-// [c_lo + y*SUB_CHUNK, +SUB_CHUNK) below c_hi, staging 256 candidate keys at a
-// time in LDS: every lane reads the same LDS address (a broadcast, no bank
-// conflicts), so one key load serves 256 tests and a candidate is read once per
-// block.  A hit clears kept[k] (all ones before the first pass); a lane also
-// stops once another block cleared its clause, the block once all lanes stopped.
-// The host runs it twice: a short prefix of the candidates for every new clause
-// (most are subsumed early), then the rest for the survivors only, so the
-// long scans run on full waves.  tests_out: subset tests performed.
-constexpr int SUB_TILE = 256, SUB_CHUNK = 4096, SUB_PREFIX = 1024;
-template <int K>
-__global__ void __launch_bounds__(SUB_TILE) dp_subsume_tiled_kernel(ClauseList L, const int64_t *rlist, int64_t nrem,
-                                                                    const uint64_t *rbits, const int64_t *ntlist,
-                                                                    const int64_t *sel, int64_t nsel, int64_t c_lo,
-                                                                    int64_t c_hi, int64_t *kept,
-                                                                    unsigned long long *tests_out) {
-    __shared__ uint64_t tile[SUB_TILE][K];
-    __shared__ unsigned long long tsum;
-    __shared__ int64_t kmax_s;
+// every survivor x against the survivors y earlier in pair order (REF.py:124,
+// unique_new part): hit[x] = epoch when some y is a subset of x
+template <int KT>
+__global__ void __launch_bounds__(TEST_TILE) dp_survtest_kernel(DpArgs A) {
+    __shared__ int wsum[4];
+    DpState *S = A.st;
+    if (S->done || S->first_empty != DP_EMPTY) return;
+    int tests = 0;
+    dp_test_items<KT, true>(A, S->nsurv, S->nsurv, A.skeys, A.skeys, A.surv, A.hit, S->epoch, tests);
+    const int tot = block_sum(tests, wsum);
+    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long *)&S->tests, (unsigned long long)tot);
+}
+
+// One workgroup: the step's verdict (the first empty resolvent, or the clause
+// limit, whichever comes first in pair order -- REF.py:117-118), else the kept
+// survivors in pair order and the capacities of the next generation.
+__global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
+    __shared__ int wsum[16];
+    __shared__ int64_t sh_lim;
+    DpState *S = A.st;
+    if (S->done) return;
     const int tid = threadIdx.x;
-    const int64_t s = (int64_t)blockIdx.x * SUB_TILE + tid;
-    const bool valid = s < nsel;
-    const int64_t k = valid ? (sel ? sel[s] : s) : 0;
-    if (tid == 0) {
-        tsum = 0;
-        kmax_s = 0;
-    }
-    __syncthreads();
-    if (valid) atomicMax((unsigned long long *)&kmax_s, (unsigned long long)k);
-    __syncthreads();
-    const int64_t c_beg = c_lo + (int64_t)blockIdx.y * SUB_CHUNK;
-    const int64_t c_end = min(min(c_beg + SUB_CHUNK, c_hi), nrem + kmax_s);   // no candidate beyond the last clause's
-    if (c_beg >= c_end) return;                                               // (block-uniform)
-    uint64_t x[K];
-#pragma unroll
-    for (int w = 0; w < K; ++w) x[w] = valid ? rbits[ntlist[k] * K + w] : 0ull;
-    const int64_t mine = valid ? nrem + k : 0;   // candidates of clause k: c < nrem + k
-    bool alive = valid && c_beg < mine;
-    uint64_t tests = 0;
-    for (int64_t e0 = c_beg; e0 < c_end; e0 += SUB_TILE) {
-        if (alive && __hip_atomic_load(&kept[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) alive = false;
-        if (!__syncthreads_or(alive)) break;
-        const int64_t e = e0 + tid;
-        if (e < c_end) {
-            const uint64_t *src = e < nrem ? L.bits + rlist[e] * K : rbits + ntlist[e - nrem] * K;
-#pragma unroll
-            for (int w = 0; w < K; ++w) tile[tid][w] = src[w];
-        }
-        __syncthreads();
-        if (alive) {
-            const int cnt = (int)(min(min(e0 + SUB_TILE, c_end), mine) - e0);
-            for (int j = 0; j < cnt; ++j) {
-                uint64_t out = 0;
-#pragma unroll
-                for (int w = 0; w < K; ++w) out |= tile[j][w] & ~x[w];
-                ++tests;
-                if (out == 0ull) {
-                    alive = false;
-                    __hip_atomic_store(&kept[k], (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t fe = S->first_empty;
+    const int64_t npairs = S->npairs, nr = S->nr, nontaut = S->nontaut;
+    // clause_limit: the reference stops when remaining + new passes the limit,
+    // i.e. at the kth non-tautological non-empty pair (0-based)
+    int64_t limit_pair = -1;
+    const int64_t kth = max<int64_t>(A.clause_limit - nr, 0);
+    if (A.clause_limit > 0 && nontaut > kth) {
+        if (tid == 0) sh_lim = -1;
+        const int64_t nw = (npairs + 63) >> 6;
+        const int64_t per = (nw + POP_THREADS - 1) / POP_THREADS;
+        const int64_t w0 = min<int64_t>(nw, tid * per), w1 = min<int64_t>(nw, w0 + per);
+        int c = 0;
+        for (int64_t w = w0; w < w1; ++w) c += __popcll(A.ntbits[w]);
+        int tot;
+        int ex = block_excl_scan(c, wsum, tot);
+        if (kth >= ex && kth < ex + c) {   // this thread's words hold the kth bit
+            int64_t need = kth - ex;
+            for (int64_t w = w0; w < w1; ++w) {
+                uint64_t m = A.ntbits[w];
+                const int pc = __popcll(m);
+                if (need < pc) {
+                    for (; need > 0; --need) m &= m - 1;
+                    sh_lim = w * 64 + __builtin_ctzll(m);
                     break;
                 }
+                need -= pc;
             }
-            if (alive && e0 + SUB_TILE >= mine) alive = false;   // this lane's candidates are done
         }
         __syncthreads();
+        limit_pair = sh_lim;
     }
-    // one atomic per block
-    atomicAdd(&tsum, (unsigned long long)tests);
-    __syncthreads();
-    if (tid == 0) atomicAdd(tests_out, tsum);
-}
-
-__global__ void dp_ones_kernel(int64_t *a, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        a[i] = 1;
-}
-
-// kept resolvent images: (pc - {var}) | (nc - {-var})  (REF.py:114)
-__global__ void dp_build_kernel(Images A, Images B, const int64_t *ntlist, const int64_t *kflag, const int64_t *kpos,
-                                int64_t m, int64_t nn, Images R, int *overflow) {
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
-        if (!kflag[k]) continue;
-        const int64_t p = ntlist[k], e = kpos[k];
-        int32_t *a = R.pool + e * 2 * R.cap;
-        DSet s;
-        dset_init(s, a, a + R.cap, R.cap);
-        py_merge(s, img_view(A, p / nn));   // set_copy(AX)
-        py_merge(s, img_view(B, p % nn));   // |= BY
-        if (s.overflow) *overflow = 1;
-        R.off[e] = s.t - R.pool;
-        R.mask[e] = (int32_t)s.mask;
-        R.fill[e] = (int32_t)s.fill;
-        R.used[e] = (int32_t)s.used;
-    }
-}
-
-__global__ void dp_sizes_kernel(ClauseList L, const int64_t *rlist, int64_t nrem, Images R, int64_t nkept,
-                                int64_t *size) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nrem + nkept;
-         t += (int64_t)gridDim.x * blockDim.x)
-        size[t] = (t < nrem ? L.mask[rlist[t]] : R.mask[t - nrem]) + 1;
-}
-
-// next generation: remaining_clauses + unique_new (REF.py:127)
-__global__ void dp_assemble_kernel(ClauseList L, const int64_t *rlist, int64_t nrem, Images R, const int64_t *klist,
-                                   int64_t nkept, const uint64_t *rbits, const int64_t *ntlist, const int64_t *off,
-                                   int K, ClauseList O) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nrem + nkept;
-         t += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t *src;
-        const uint64_t *bsrc;
-        int32_t mask, fill, used;
-        if (t < nrem) {
-            const int64_t c = rlist[t];
-            src = L.pool + L.off[c];
-            bsrc = L.bits + c * K;
-            mask = L.mask[c];
-            fill = L.fill[c];
-            used = L.used[c];
-        } else {
-            const int64_t e = t - nrem;
-            src = R.pool + R.off[e];
-            bsrc = rbits + ntlist[klist[e]] * K;
-            mask = R.mask[e];
-            fill = R.fill[e];
-            used = R.used[e];
+    if (fe != DP_EMPTY || limit_pair >= 0) {
+        if (tid == 0) {
+            S->result = (fe != DP_EMPTY && (limit_pair < 0 || (int64_t)fe < limit_pair)) ? 0 : -1;
+            S->done = 1;
         }
-        int32_t *dst = O.pool + off[t];
-        for (int32_t i = 0; i <= mask; ++i) dst[i] = src[i];
-        for (int w = 0; w < K; ++w) O.bits[t * K + w] = bsrc[w];
-        O.off[t] = off[t];
-        O.mask[t] = mask;
-        O.fill[t] = fill;
-        O.used[t] = used;
+        return;
     }
+    const int64_t ns = S->nsurv;
+    const int32_t epoch = S->epoch;
+    int kc = 0;
+    for (int64_t i = tid; i < ns; i += POP_THREADS) kc += A.hit[i] != epoch ? 1 : 0;
+    const int nkept = block_sum(kc, wsum);
+    const int64_t ncl2 = nr + nkept;
+    const int64_t capA = S->capA, capB = S->capB, capR = S->capR;
+    const int64_t arena_need = S->arena_top + (int64_t)nkept * 2 * capR;
+    const int64_t xs_need = (int64_t)nkept * 2 * (capA + capB);
+    int ovf = 0;
+    if (ncl2 > A.ncl_cap) ovf |= OVF_NCL;
+    if (arena_need > A.arena_cap) ovf |= OVF_ARENA;
+    if (xs_need > A.xs_cap) ovf |= OVF_XS;
+    if (ovf) {   // grow and run this step again (its input generation is untouched)
+        if (tid == 0) {
+            S->need[1] = ncl2;
+            S->need[2] = arena_need;
+            S->need[3] = xs_need;
+            S->overflow |= ovf;
+            S->steps -= 1;
+            S->done = 1;
+        }
+        return;
+    }
+    for (int64_t i = tid; i < ns; i += POP_THREADS)
+        if (A.hit[i] != epoch) {
+            const uint32_t p = A.surv[i];
+            atomicOr(A.keptbits + (p >> 5), 1u << (p & 31));
+        }
+    __syncthreads();
+    // ordered compaction of the kept bitmap (words cleared as read)
+    const int64_t nw = (npairs + 31) >> 5;
+    const int64_t per = (nw + POP_THREADS - 1) / POP_THREADS;
+    const int64_t w0 = min<int64_t>(nw, tid * per), w1 = min<int64_t>(nw, w0 + per);
+    int c = 0;
+    for (int64_t w = w0; w < w1; ++w)
+        c += __popc(__hip_atomic_load(A.keptbits + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    int tot;
+    int pos = block_excl_scan(c, wsum, tot);
+    for (int64_t w = w0; w < w1; ++w) {
+        uint32_t m = __hip_atomic_load(A.keptbits + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!m) continue;
+        A.keptbits[w] = 0u;
+        while (m) {
+            A.klist[pos++] = (uint32_t)(w * 32 + __builtin_ctz(m));
+            m &= m - 1;
+        }
+    }
+    if (tid == 0) {
+        S->nkept = nkept;
+        S->ncl2 = ncl2;
+        S->arena_base = S->arena_top;
+        S->arena_top = arena_need;
+        S->new_total += nontaut;
+        S->pending = 1;
+    }
+}
+
+// clauses = remaining_clauses + unique_new (REF.py:127): one wavefront per
+// clause of the next list.  A rem clause keeps its image; kept resolvent k =
+// pair (i, j) gets the image of (pc - {var}) | (nc - {-var}) (REF.py:114),
+// built by lane 0 -- CPython's insertions are a serial chain of dependent
+// probes -- in the wave's LDS scratch when the step's capacities fit it (else
+// in HBM scratch), then copied to the arena at arena_base + 2*capR*k by the
+// whole wave.  The lanes then read the clause's table slots at once for the
+// next step's first-position table.
+constexpr int ASM_WAVES = 4, ASM_SCRATCH = 1024;   // per wave: int32 slots of AX, BY and R tables
+__global__ void __launch_bounds__(64 * ASM_WAVES) dp_assemble_kernel(DpArgs A) {
+    __shared__ unsigned long long lfp_sh[FP_LDS];
+    __shared__ int32_t scratch_sh[ASM_WAVES][ASM_SCRATCH];
+    DpState *S = A.st;
+    if (S->done) return;
+    unsigned long long *lfp = A.V <= FP_LDS ? lfp_sh : nullptr;
+    firstpos_begin(A, lfp);
+    const int cur = S->cur;
+    const ClauseList L = A.g[cur], O = A.g[cur ^ 1];
+    const int64_t ncl2 = S->ncl2, nr = S->nr, nn = S->nn, base = S->arena_base;
+    const int64_t capA = S->capA, capB = S->capB, capR = S->capR;
+    const int32_t var = S->var;
+    const int K = A.K, lane = lane_id(), wid = threadIdx.x >> 6;
+    const bool lds_ok = 2 * (capA + capB + capR) <= ASM_SCRATCH;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < ncl2; t += nwaves) {
+        const int32_t *img;
+        int64_t mask;
+        if (t < nr) {
+            const int64_t c = A.rlist[t];
+            mask = L.mask[c];
+            if (lane == 0) {
+                O.off[t] = L.off[c];
+                O.mask[t] = (int32_t)mask;
+                O.fill[t] = L.fill[c];
+                O.used[t] = L.used[c];
+            }
+            if (lane < K) O.bits[t * K + lane] = L.bits[c * K + lane];
+            img = A.arena + L.off[c];
+        } else {
+            const int64_t k = t - nr;
+            const uint32_t p = A.klist[k];
+            int32_t *xa = lds_ok ? scratch_sh[wid] : A.xs + k * 2 * (capA + capB);
+            int32_t *xb = xa + 2 * capA;
+            int32_t *dst = A.arena + base + k * 2 * capR;
+            int32_t *ra = lds_ok ? xb + 2 * capB : dst;
+            int64_t rm = 0, rf = 0, ru = 0, roff = 0;
+            if (lane == 0) {
+                const uint32_t i = p / (uint32_t)nn, j = p - i * (uint32_t)nn;
+                DSet ax, by, r;
+                dset_init(ax, xa, xa + capA, capA);
+                py_difference1(ax, cl_view(L, A.arena, A.plist[i]), var);    // pc - {var}
+                dset_init(by, xb, xb + capB, capB);
+                py_difference1(by, cl_view(L, A.arena, A.nlist[j]), -var);   // nc - {-var}
+                dset_init(r, ra, ra + capR, capR);
+                py_merge(r, dset_view(ax));   // set_copy(AX)
+                py_merge(r, dset_view(by));   // |= BY
+                if (ax.overflow || by.overflow || r.overflow) S->set_ovf = 1;
+                rm = r.mask;
+                rf = r.fill;
+                ru = r.used;
+                roff = r.t - ra;
+            }
+            wave_sync();
+            rm = __shfl(rm, 0);
+            rf = __shfl(rf, 0);
+            ru = __shfl(ru, 0);
+            roff = __shfl(roff, 0);
+            const int32_t *src = ra + roff;
+            int32_t *out = lds_ok ? dst : ra + roff;
+            if (lds_ok)
+                for (int64_t x = lane; x <= rm; x += 64) dst[x] = src[x];
+            if (lane == 0) {
+                O.off[t] = out - A.arena;
+                O.mask[t] = (int32_t)rm;
+                O.fill[t] = (int32_t)rf;
+                O.used[t] = (int32_t)ru;
+            }
+            if (lane < K) O.bits[t * K + lane] = A.rbits[(uint64_t)p * K + lane];
+            img = src;
+            mask = rm;
+        }
+        for (int64_t x = lane; x <= mask; x += 64) {   // first positions (REF.py:128's comprehension order)
+            const int32_t key = img[x];
+            if (key == PY_EMPTY || key == PY_DUMMY) continue;
+            const int d = A.v2d[key < 0 ? -key : key];
+            const unsigned long long pos = ((unsigned long long)t << 32) | (unsigned long long)x;
+            if (lfp)
+                atomicMin(&lfp[d], pos);
+            else
+                atomicMin(&A.firstpos[d], pos);
+        }
+        wave_sync();   // the wave's scratch is rewritten by its next clause
+    }
+    firstpos_flush(A, lfp);
 }
 
 // ------------------------------------------------------------------ host side
@@ -406,13 +842,26 @@ struct Buf {
     }
     Buf() = default;
     Buf(const Buf &) = delete;
-    int need(size_t bytes) {
+    // grow to >= bytes; keep the first `keep` bytes (stream-ordered copy); `fill`
+    // (>= 0) initialises the whole new buffer first
+    int need(size_t bytes, hipStream_t s = nullptr, size_t keep = 0, int fill = -1) {
         if (bytes <= cap) return SATMI_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
         const size_t want = std::max<size_t>(bytes + bytes / 2, 256);
-        SATMI_HIP(hipMalloc(&p, want));
+        void *np = nullptr;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && want > free_b) {
+            set_error("satmi_dp_host: out of device memory (" + std::to_string(want >> 20) + " MiB wanted, " +
+                      std::to_string(free_b >> 20) + " MiB free); bound the elimination with clause_limit");
+            return SATMI_ERR_NOMEM;
+        }
+        SATMI_HIP(hipMalloc(&np, want));
+        if (fill >= 0) SATMI_HIP(hipMemsetAsync(np, fill, want, s));
+        if (p && keep) SATMI_HIP(hipMemcpyAsync(np, p, std::min(keep, cap), hipMemcpyDeviceToDevice, s));
+        if (p) {
+            SATMI_HIP(hipStreamSynchronize(s));   // the old buffer is no longer read
+            (void)hipFree(p);
+        }
+        p = np;
         cap = want;
         return SATMI_OK;
     }
@@ -426,44 +875,23 @@ struct Buf {
         if (_rc != SATMI_OK) return _rc; \
     } while (0)
 
-struct Gen {   // one generation of the clause list
-    Buf off, mask, fill, used, bits, pool;
-    int reserve(int64_t n, int K, int64_t pool_slots) {
-        DP_TRY(off.need(8 * (size_t)std::max<int64_t>(n, 1)));
-        DP_TRY(mask.need(4 * (size_t)std::max<int64_t>(n, 1)));
-        DP_TRY(fill.need(4 * (size_t)std::max<int64_t>(n, 1)));
-        DP_TRY(used.need(4 * (size_t)std::max<int64_t>(n, 1)));
-        DP_TRY(bits.need(8 * (size_t)std::max<int64_t>(n, 1) * K));
-        DP_TRY(pool.need(4 * (size_t)std::max<int64_t>(pool_slots, 1)));
+struct Gen {   // one generation's per-clause arrays
+    Buf off, mask, fill, used, bits;
+    int reserve(int64_t n, int K, hipStream_t s, int64_t keep_n) {
+        n = std::max<int64_t>(n, 1);
+        DP_TRY(off.need(8 * (size_t)n, s, 8 * (size_t)keep_n));
+        DP_TRY(mask.need(4 * (size_t)n, s, 4 * (size_t)keep_n));
+        DP_TRY(fill.need(4 * (size_t)n, s, 4 * (size_t)keep_n));
+        DP_TRY(used.need(4 * (size_t)n, s, 4 * (size_t)keep_n));
+        DP_TRY(bits.need(8 * (size_t)n * K, s, 8 * (size_t)keep_n * K));
         return SATMI_OK;
     }
     ClauseList view() const {
-        return {off.as<int64_t>(), mask.as<int32_t>(), fill.as<int32_t>(), used.as<int32_t>(), bits.as<uint64_t>(),
-                pool.as<int32_t>()};
+        return {off.as<int64_t>(), mask.as<int32_t>(), fill.as<int32_t>(), used.as<int32_t>(), bits.as<uint64_t>()};
     }
 };
 
-struct Img {
-    Buf pool, off, mask, fill, used;
-    int64_t cap = 8;
-    int reserve(int64_t n, int64_t c) {
-        cap = c;
-        n = std::max<int64_t>(n, 1);
-        DP_TRY(pool.need(4 * (size_t)n * 2 * c));
-        DP_TRY(off.need(8 * (size_t)n));
-        DP_TRY(mask.need(4 * (size_t)n));
-        DP_TRY(fill.need(4 * (size_t)n));
-        DP_TRY(used.need(4 * (size_t)n));
-        return SATMI_OK;
-    }
-    Images view() const {
-        return {pool.as<int32_t>(), off.as<int64_t>(), mask.as<int32_t>(), fill.as<int32_t>(), used.as<int32_t>(),
-                cap};
-    }
-};
-
-// Work and device time of the last satmi_dp_host call's subsumption filter
-// (HIP events on its stream), for bench.py's roofline.
+// Work and device time of the last satmi_dp_host call, for bench.py's roofline.
 struct DpStats {
     int64_t steps = 0, tests = 0, new_clauses = 0, candidates_bytes = 0;
     double subsume_ms = 0.0;
@@ -471,69 +899,141 @@ struct DpStats {
 };
 thread_local DpStats g_dp_stats;   // the calling thread's last call
 
-// Everything one satmi_dp_host call allocates, kept between calls (grow-only)
-// per host thread and device, with the thread's own non-blocking stream: a
-// solve of a small formula is dozens of steps of small launches with a few
-// host read-backs each, so allocating its ~40 buffers per call cost more than
-// its kernels, and solves from several host threads overlap on the device
-// (each fills a fraction of it).  Never destroyed: no hipFree after the
-// runtime's teardown.
+// Device buffers of one solve, kept between calls (grow-only) in a process-wide
+// pool: a call takes a free workspace (or makes one) and returns it when done,
+// so concurrent calls from any number of threads each own one and the number
+// of workspaces is the peak number of concurrent calls.
 struct DpWork {
-    Buf d_off, d_lits, d_v2d, d_d2v, misc, firstpos, order, popscratch, base, usedtmp;
-    Buf fpos, fneg, frem, plist, nlist, rlist, scanpos, tiles, grand, counts3, rbits, nontaut, ntlist, kept, klist, kpos,
-        sizes, offs;
+    Buf d_off, d_lits, d_v2d, d_d2v, state, firstpos, order, popscratch, trace;
+    Buf plist, nlist, rlist, rbits, ntbits, table, uslot, dropped, hit, surv, klist, keptbits, xs, arena;
+    Buf rkeys, ukeys, skeys;
     Gen g[2];
-    Img A, B, R;
-    std::vector<hipEvent_t> ev;   // subsumption-filter timing: one pair per step, read once per call
+    int64_t ncl_cap = 0, pair_cap = 0, arena_cap = 0, xs_cap = 0;
+    uint64_t tslots = 0;
+    int K = 0;
+    int32_t epoch = 0;
+    std::vector<hipEvent_t> ev;   // filter timing: one pair per step, read once per call
     hipStream_t stream = nullptr;
-    int64_t *pin = nullptr;       // pinned host word: a step's pool size, read after the next step's first wait
-};
-DpWork *dp_work(int dev) {
-    thread_local std::vector<DpWork *> mine;
-    if ((int)mine.size() <= dev) mine.resize(dev + 1, nullptr);
-    if (!mine[dev]) {
-        DpWork *w = new DpWork;
-        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
-            hipHostMalloc((void **)&w->pin, 64, hipHostMallocDefault) != hipSuccess) {
-            delete w;
-            return nullptr;
-        }
-        mine[dev] = w;
+    DpState *pin = nullptr;       // pinned host copy of the state
+    int dev = 0;
+    ~DpWork() {   // only a workspace that failed mid-call is destroyed (after its stream drained)
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+        if (pin) (void)hipHostFree(pin);
     }
-    return mine[dev];
-}
+};
 
-// ordered compaction of flag[n] into out (indices); returns the count
-// compact() without the count read-back: `out` is sized for all n, the count
-// lands in *count_dev; several of these share one read-back (same stream, so
-// pos / tiles are reused in order)
-int compact_deferred(const int64_t *flag, int64_t n, Buf &pos, Buf &tiles, int64_t *count_dev, Buf &out,
-                     hipStream_t s) {
-    DP_TRY(pos.need(8 * (size_t)std::max<int64_t>(n, 1)));
-    DP_TRY(tiles.need(8 * (size_t)((n + SCAN_TILE - 1) / SCAN_TILE + 1)));
-    DP_TRY(out.need(8 * (size_t)std::max<int64_t>(n, 1)));
-    DP_TRY(exclusive_scan(flag, pos.as<int64_t>(), n, tiles.as<int64_t>(), count_dev, s));
-    if (n > 0)
-        hipLaunchKernelGGL(dp_compact_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, flag, pos.as<int64_t>(), n,
-                           out.as<int64_t>());
-    SATMI_HIP(hipGetLastError());
+struct DpPool {
+    std::mutex mu;
+    std::vector<DpWork *> free_list;
+};
+DpPool &dp_pool() {
+    static DpPool *p = new DpPool;   // never destroyed: no hipFree after the runtime's teardown
+    return *p;
+}
+DpWork *dp_acquire(int dev) {
+    DpPool &P = dp_pool();
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        for (size_t i = 0; i < P.free_list.size(); ++i)
+            if (P.free_list[i]->dev == dev) {
+                DpWork *w = P.free_list[i];
+                P.free_list.erase(P.free_list.begin() + (long)i);
+                return w;
+            }
+    }
+    DpWork *w = new DpWork;
+    w->dev = dev;
+    if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&w->pin, sizeof(DpState), hipHostMallocDefault) != hipSuccess) {
+        delete w;
+        return nullptr;
+    }
+    return w;
+}
+void dp_release(DpWork *w) {
+    DpPool &P = dp_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    P.free_list.push_back(w);
+}
+// A call's hold on a workspace: returned to the pool after a call that
+// completed; destroyed after a call that failed part-way (its device state --
+// epoch stamps, the hash table -- may not be clean).
+struct DpLease {
+    DpWork *w;
+    bool ok = false;
+    ~DpLease() {
+        if (!w) return;
+        if (ok) {
+            dp_release(w);
+        } else {
+            (void)hipStreamSynchronize(w->stream);
+            delete w;
+        }
+    }
+};
+
+// grow the pair-sized buffers (contents are per-step scratch; the stamp
+// arrays start at 0, the table EMPTY, the kept bitmap clear)
+int grow_pairs(DpWork &W, int64_t npairs, int K) {
+    if (npairs <= W.pair_cap && W.K == K && W.tslots) return SATMI_OK;
+    const int64_t cap = std::max<int64_t>(std::max<int64_t>(npairs + npairs / 2, 1 << 16), W.pair_cap);
+    if (cap >= (1ll << 31)) {
+        set_error("satmi_dp_host: more than 2^31 resolvent pairs in one step");
+        return SATMI_ERR_TOO_LARGE;
+    }
+    hipStream_t s = W.stream;
+    DP_TRY(W.rbits.need(8 * (size_t)cap * K, s));
+    DP_TRY(W.ntbits.need(8 * (size_t)((cap + 63) / 64 + 1), s));
+    DP_TRY(W.uslot.need(4 * (size_t)cap, s));
+    DP_TRY(W.surv.need(4 * (size_t)cap, s));
+    DP_TRY(W.klist.need(4 * (size_t)cap, s));
+    DP_TRY(W.ukeys.need(8 * (size_t)cap * K, s));
+    DP_TRY(W.skeys.need(8 * (size_t)cap * K, s));
+    DP_TRY(W.dropped.need(4 * (size_t)cap, s, 0, 0));
+    DP_TRY(W.hit.need(4 * (size_t)cap, s, 0, 0));
+    DP_TRY(W.keptbits.need(4 * (size_t)((cap + 31) / 32 + 1), s, 0, 0));
+    uint64_t ts = 1024;
+    while (ts < 2 * (uint64_t)cap) ts <<= 1;
+    DP_TRY(W.table.need(8 * (size_t)ts, s, 0, 0xFF));
+    // a buffer that did not move keeps its contents: the stamps stay below
+    // the next epoch, every step leaves the bitmap and the table clear (slots
+    // past the old table size were never used)
+    uint64_t pw = 1024;
+    while (pw * 2 <= W.table.cap / 8) pw <<= 1;
+    W.tslots = pw;
+    W.pair_cap = std::min<int64_t>((int64_t)(W.rbits.cap / (8 * (size_t)K)), (int64_t)(W.tslots / 2));
+    W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.uslot.cap / 4));
+    W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.ukeys.cap / (8 * (size_t)K)));
+    W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.skeys.cap / (8 * (size_t)K)));
+    W.pair_cap = std::min<int64_t>(W.pair_cap, (1ll << 31) - 1);
+    W.K = K;
     return SATMI_OK;
 }
 
-int compact(const int64_t *flag, int64_t n, Buf &pos, Buf &tiles, Buf &grand, Buf &out, int64_t *count,
-            hipStream_t s) {
-    *count = 0;
-    if (n == 0) return SATMI_OK;
-    DP_TRY(pos.need(8 * (size_t)n));
-    DP_TRY(tiles.need(8 * (size_t)((n + SCAN_TILE - 1) / SCAN_TILE + 1)));
-    DP_TRY(grand.need(8));
-    DP_TRY(exclusive_scan(flag, pos.as<int64_t>(), n, tiles.as<int64_t>(), grand.as<int64_t>(), s));
-    SATMI_HIP(hipMemcpyAsync(count, grand.p, 8, hipMemcpyDeviceToHost, s));
-    SATMI_HIP(hipStreamSynchronize(s));
-    DP_TRY(out.need(8 * (size_t)std::max<int64_t>(*count, 1)));
-    hipLaunchKernelGGL(dp_compact_kernel, dim3(grid_for(n)), dim3(PRIM_BLOCK), 0, s, flag, pos.as<int64_t>(), n,
-                       out.as<int64_t>());
-    SATMI_HIP(hipGetLastError());
+int grow_ncl(DpWork &W, int64_t n, int K, int cur, int64_t keep_n) {
+    if (n <= W.ncl_cap && W.K == K) return SATMI_OK;
+    hipStream_t s = W.stream;
+    const int64_t cap = std::max<int64_t>(n + n / 2, 1024);
+    DP_TRY(W.g[cur].reserve(cap, K, s, keep_n));
+    DP_TRY(W.g[cur ^ 1].reserve(cap, K, s, 0));
+    DP_TRY(W.plist.need(8 * (size_t)cap, s));
+    DP_TRY(W.nlist.need(8 * (size_t)cap, s));
+    DP_TRY(W.rlist.need(8 * (size_t)cap, s));
+    DP_TRY(W.rkeys.need(8 * (size_t)cap * K, s));
+    int64_t c = INT64_MAX;
+    for (int g = 0; g < 2; ++g) {
+        c = std::min<int64_t>(c, (int64_t)(W.g[g].off.cap / 8));
+        c = std::min<int64_t>(c, (int64_t)(W.g[g].mask.cap / 4));
+        c = std::min<int64_t>(c, (int64_t)(W.g[g].fill.cap / 4));
+        c = std::min<int64_t>(c, (int64_t)(W.g[g].used.cap / 4));
+        c = std::min<int64_t>(c, (int64_t)(W.g[g].bits.cap / (8 * (size_t)K)));
+    }
+    c = std::min<int64_t>(c, (int64_t)(W.plist.cap / 8));
+    c = std::min<int64_t>(c, (int64_t)(W.nlist.cap / 8));
+    c = std::min<int64_t>(c, (int64_t)(W.rlist.cap / 8));
+    c = std::min<int64_t>(c, (int64_t)(W.rkeys.cap / (8 * (size_t)K)));
+    W.ncl_cap = c;
     return SATMI_OK;
 }
 
@@ -551,7 +1051,6 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         set_error("satmi_dp_host: bad arguments");
         return SATMI_ERR_ARG;
     }
-    const auto t_start = std::chrono::steady_clock::now();
     *h_result = -1;
     *h_steps = 0;
     if (h_rec_step_off && rec_step_cap > 0) h_rec_step_off[0] = 0;
@@ -574,56 +1073,113 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             dense2var.push_back(v);
         }
     const int V = (int)dense2var.size();
-    const int W = std::max(1, (V + 63) / 64);
-    const int K = 2 * W;
+    g_dp_stats = DpStats{};
+    if (V == 0) {   // no variables: `while variables` never runs -- True (REF.py:130)
+        *h_result = 1;
+        return SATMI_OK;
+    }
+    const int Wd = (V + 63) / 64;
+    const int K = 2 * Wd;
+    g_dp_stats.words = K;
     int dev_id = 0;
     SATMI_HIP(hipGetDevice(&dev_id));
-    DpWork *wk = dp_work(dev_id);
-    if (!wk) {
+    DpLease lease{dp_acquire(dev_id)};
+    if (!lease.w) {
         set_error("satmi_dp_host: hipStreamCreate failed");
         return SATMI_ERR_HIP;
     }
-    DpWork &Wk = *wk;
+    DpWork &Wk = *lease.w;
     hipStream_t s = Wk.stream;
-    Buf &d_off = Wk.d_off, &d_lits = Wk.d_lits, &d_v2d = Wk.d_v2d, &d_d2v = Wk.d_d2v, &misc = Wk.misc,
-        &firstpos = Wk.firstpos, &order = Wk.order, &popscratch = Wk.popscratch, &base = Wk.base,
-        &usedtmp = Wk.usedtmp;
-    Buf &fpos = Wk.fpos, &fneg = Wk.fneg, &frem = Wk.frem, &plist = Wk.plist, &nlist = Wk.nlist, &rlist = Wk.rlist,
-        &scanpos = Wk.scanpos, &tiles = Wk.tiles, &grand = Wk.grand, &counts3 = Wk.counts3, &rbits = Wk.rbits,
-        &nontaut = Wk.nontaut, &ntlist = Wk.ntlist, &kept = Wk.kept, &klist = Wk.klist, &kpos = Wk.kpos,
-        &sizes = Wk.sizes, &offs = Wk.offs;
-    Gen *g = Wk.g;
-    Img &A = Wk.A, &B = Wk.B, &R = Wk.R;
-    DP_TRY(d_off.need(4 * (size_t)(nclauses + 1)));
-    DP_TRY(d_lits.need(4 * (size_t)std::max<int64_t>(Ltot, 1)));
-    DP_TRY(d_v2d.need(4 * (size_t)(maxvar + 1)));
-    DP_TRY(d_d2v.need(4 * (size_t)std::max(V, 1)));
-    DP_TRY(misc.need(64));
-    int cur = 0;
-    int64_t ncl = nclauses;
-    int64_t pool_cur = 0;         // pool slots of g[cur] (exact, or this step's bound until read back)
-    bool pool_pending = false;    // Wk.pin[0] holds g[cur]'s exact pool size after the next wait
-    {
-        const int64_t cap0 = cap_for(maxlen);
-        pool_cur = ncl * 2 * cap0;
-        DP_TRY(g[0].reserve(ncl, K, pool_cur));
-        if (nclauses > 0) {
-            SATMI_HIP(hipMemcpyAsync(d_off.p, h_clause_off, 4 * (size_t)(nclauses + 1), hipMemcpyHostToDevice, s));
-            if (Ltot) SATMI_HIP(hipMemcpyAsync(d_lits.p, h_lits, 4 * (size_t)Ltot, hipMemcpyHostToDevice, s));
-            SATMI_HIP(hipMemcpyAsync(d_v2d.p, var2dense.data(), 4 * (size_t)(maxvar + 1), hipMemcpyHostToDevice, s));
-        }
-        if (V) SATMI_HIP(hipMemcpyAsync(d_d2v.p, dense2var.data(), 4 * (size_t)V, hipMemcpyHostToDevice, s));
-        SATMI_HIP(hipMemsetAsync(misc.p, 0, 64, s));
-        if (nclauses > 0) {
-            hipLaunchKernelGGL(dp_encode_kernel, dim3(grid_for(nclauses)), dim3(PRIM_BLOCK), 0, s, nclauses,
-                               d_off.as<int32_t>(), d_lits.as<int32_t>(), d_v2d.as<int32_t>(), W, cap0,
-                               g[0].view(), misc.as<int>());
-            SATMI_HIP(hipGetLastError());
-        }
+    if (Wk.K != K) {   // key width changed: every K-sized buffer is re-laid out
+        Wk.ncl_cap = 0;
+        Wk.pair_cap = 0;
     }
-    // subsumption-filter timing (satmi_dp_last_stats): an event pair per step,
-    // read after the loop (no per-step wait); misc[40..48) counts its subset tests
-    size_t nev = 0;   // event pairs recorded this call
+    const int64_t cap0 = cap_for(maxlen);
+    DP_TRY(Wk.d_off.need(4 * (size_t)(nclauses + 1), s));
+    DP_TRY(Wk.d_lits.need(4 * (size_t)std::max<int64_t>(Ltot, 1), s));
+    DP_TRY(Wk.d_v2d.need(4 * (size_t)(maxvar + 1), s));
+    DP_TRY(Wk.d_d2v.need(4 * (size_t)V, s));
+    DP_TRY(Wk.state.need(sizeof(DpState), s));
+    DP_TRY(Wk.firstpos.need(8 * (size_t)V, s));
+    DP_TRY(Wk.order.need(4 * (size_t)V, s));
+    const int64_t popcap = cap_for(V);
+    DP_TRY(Wk.popscratch.need(4 * (size_t)2 * popcap, s));
+    DP_TRY(Wk.trace.need(4 * (size_t)(V + 1), s));
+    DP_TRY(grow_ncl(Wk, std::max<int64_t>(nclauses, 1), K, 0, 0));
+    DP_TRY(grow_pairs(Wk, 1, K));
+    const int64_t arena0 = (int64_t)nclauses * 2 * cap0;
+    DP_TRY(Wk.arena.need(4 * (size_t)std::max<int64_t>(arena0 * 4, 1 << 16), s));
+    Wk.arena_cap = (int64_t)(Wk.arena.cap / 4);
+    DP_TRY(Wk.xs.need(4 * (size_t)(1 << 16), s));
+    Wk.xs_cap = (int64_t)(Wk.xs.cap / 4);
+
+    if (nclauses > 0) {
+        SATMI_HIP(hipMemcpyAsync(Wk.d_off.p, h_clause_off, 4 * (size_t)(nclauses + 1), hipMemcpyHostToDevice, s));
+        if (Ltot) SATMI_HIP(hipMemcpyAsync(Wk.d_lits.p, h_lits, 4 * (size_t)Ltot, hipMemcpyHostToDevice, s));
+    }
+    SATMI_HIP(hipMemcpyAsync(Wk.d_v2d.p, var2dense.data(), 4 * (size_t)(maxvar + 1), hipMemcpyHostToDevice, s));
+    SATMI_HIP(hipMemcpyAsync(Wk.d_d2v.p, dense2var.data(), 4 * (size_t)V, hipMemcpyHostToDevice, s));
+    SATMI_HIP(hipMemsetAsync(Wk.firstpos.p, 0xFF, 8 * (size_t)V, s));
+    DpState &st = *Wk.pin;
+    st = DpState{};
+    st.ncl = nclauses;
+    st.arena_top = arena0;
+    st.first_empty = DP_EMPTY;
+    st.epoch = Wk.epoch;
+    SATMI_HIP(hipMemcpyAsync(Wk.state.p, Wk.pin, sizeof(DpState), hipMemcpyHostToDevice, s));
+
+    double hz = 1e8;
+    (void)satmi_wallclock_hz(&hz);
+    const auto args = [&]() {
+        DpArgs a;
+        a.st = Wk.state.as<DpState>();
+        a.g[0] = Wk.g[0].view();
+        a.g[1] = Wk.g[1].view();
+        a.arena = Wk.arena.as<int32_t>();
+        a.arena_cap = Wk.arena_cap;
+        a.v2d = Wk.d_v2d.as<int32_t>();
+        a.d2v = Wk.d_d2v.as<int32_t>();
+        a.V = V;
+        a.W = Wd;
+        a.K = K;
+        a.firstpos = Wk.firstpos.as<unsigned long long>();
+        a.order = Wk.order.as<int32_t>();
+        a.popscratch = Wk.popscratch.as<int32_t>();
+        a.popcap = popcap;
+        a.plist = Wk.plist.as<int64_t>();
+        a.nlist = Wk.nlist.as<int64_t>();
+        a.rlist = Wk.rlist.as<int64_t>();
+        a.ncl_cap = Wk.ncl_cap;
+        a.rbits = Wk.rbits.as<uint64_t>();
+        a.ntbits = Wk.ntbits.as<uint64_t>();
+        a.pair_cap = Wk.pair_cap;
+        a.table = Wk.table.as<uint64_t>();
+        a.tmask = Wk.tslots - 1;
+        a.uslot = Wk.uslot.as<uint32_t>();
+        a.dropped = Wk.dropped.as<int32_t>();
+        a.hit = Wk.hit.as<int32_t>();
+        a.surv = Wk.surv.as<uint32_t>();
+        a.klist = Wk.klist.as<uint32_t>();
+        a.rkeys = Wk.rkeys.as<uint64_t>();
+        a.ukeys = Wk.ukeys.as<uint64_t>();
+        a.skeys = Wk.skeys.as<uint64_t>();
+        a.keptbits = Wk.keptbits.as<uint32_t>();
+        a.xs = Wk.xs.as<int32_t>();
+        a.xs_cap = Wk.xs_cap;
+        a.trace = Wk.trace.as<int32_t>();
+        a.trace_cap = V + 1;
+        a.step_limit = step_limit;
+        a.clause_limit = clause_limit;
+        a.limit_ticks = time_limit_s > 0 ? (uint64_t)std::max(1.0, time_limit_s * hz) : 0;
+        return a;
+    };
+    DpArgs A = args();
+    if (nclauses > 0) {
+        hipLaunchKernelGGL(dp_encode_kernel, dim3(grid_for(nclauses)), dim3(256), 0, s, A, nclauses,
+                           Wk.d_off.as<int32_t>(), Wk.d_lits.as<int32_t>(), cap0);
+        SATMI_HIP(hipGetLastError());
+    }
+    size_t nev = 0;   // filter timing event pairs recorded this call
     const auto next_events = [&]() -> hipEvent_t * {
         if (2 * nev + 2 > Wk.ev.size()) {
             hipEvent_t a = nullptr, b = nullptr;
@@ -633,257 +1189,129 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         }
         return &Wk.ev[2 * nev++];
     };
-    g_dp_stats = DpStats{};
-    g_dp_stats.words = K;
-    DP_TRY(firstpos.need(8 * (size_t)std::max(V, 1)));
-    DP_TRY(order.need(4 * (size_t)std::max(V, 1)));
-    const int64_t popcap = cap_for(V);
-    DP_TRY(popscratch.need(4 * (size_t)2 * popcap));
-    int steps = 0, result = 1;
-    int64_t rec_clauses = 0, rec_lits = 0;
-    std::vector<int32_t> h_pool;
-    std::vector<int64_t> h_off;
-    std::vector<int32_t> h_mask;
-    for (;;) {
-        // variables = {abs(lit) ...}; while variables: var = variables.pop()
-        if (ncl == 0) break;   // no clauses, no variables: True
-        ClauseList Lc = g[cur].view();
-        DP_TRY(base.need(8 * (size_t)ncl));
-        DP_TRY(usedtmp.need(8 * (size_t)ncl));
-        DP_TRY(tiles.need(8 * (size_t)((ncl + SCAN_TILE - 1) / SCAN_TILE + 1)));
-        DP_TRY(grand.need(8));
-        hipLaunchKernelGGL(dp_used_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, Lc, ncl,
-                           usedtmp.as<int64_t>());
-        DP_TRY(exclusive_scan(usedtmp.as<int64_t>(), base.as<int64_t>(), ncl, tiles.as<int64_t>(),
-                              grand.as<int64_t>(), s));
-        SATMI_HIP(hipMemsetAsync(firstpos.p, 0xff, 8 * (size_t)std::max(V, 1), s));
-        hipLaunchKernelGGL(dp_firstpos_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, Lc, ncl,
-                           base.as<int64_t>(), d_v2d.as<int32_t>(), firstpos.as<unsigned long long>());
-        hipLaunchKernelGGL(dp_pop_kernel, dim3(1), dim3(256), 0, s, firstpos.as<unsigned long long>(),
-                           d_d2v.as<int32_t>(), V, order.as<int32_t>(), popscratch.as<int32_t>(), popcap,
-                           misc.as<int32_t>() + 4);
+    // one elimination step: eight launches, sizes on the device
+    const auto enqueue_step = [&](const DpArgs &a) -> int {
+        const int gp = (int)std::min<int64_t>(1024, (a.pair_cap + 255) / 256);
+        const int gc = (int)std::min<int64_t>(2048, (a.ncl_cap + ASM_WAVES - 1) / ASM_WAVES);
+        hipLaunchKernelGGL(dp_pop_split_kernel, dim3(1), dim3(POP_THREADS), 0, s, a);
+        hipLaunchKernelGGL(dp_pairs_kernel, dim3(gp), dim3(256), 0, s, a);
+        hipEvent_t *ev = next_events();
+        if (!ev) {
+            set_error("satmi_dp_host: hipEventCreate failed");
+            return SATMI_ERR_HIP;
+        }
+        SATMI_HIP(hipEventRecord(ev[0], s));
+        hipLaunchKernelGGL(dp_hash_kernel, dim3(gp), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(dp_gather_kernel, dim3(gp), dim3(256), 0, s, a);
+        const dim3 gt((unsigned)std::min<int64_t>(2048, std::max<int64_t>(64, a.pair_cap / 256)));
+        switch (a.K) {
+            case 2: hipLaunchKernelGGL(dp_remtest_kernel<2>, gt, dim3(TEST_TILE), 0, s, a); break;
+            case 4: hipLaunchKernelGGL(dp_remtest_kernel<4>, gt, dim3(TEST_TILE), 0, s, a); break;
+            case 6: hipLaunchKernelGGL(dp_remtest_kernel<6>, gt, dim3(TEST_TILE), 0, s, a); break;
+            case 8: hipLaunchKernelGGL(dp_remtest_kernel<8>, gt, dim3(TEST_TILE), 0, s, a); break;
+            default: hipLaunchKernelGGL(dp_remtest_kernel<0>, gt, dim3(TEST_TILE), 0, s, a);
+        }
+        hipLaunchKernelGGL(dp_survlist_kernel, dim3(gp), dim3(256), 0, s, a);
+        switch (a.K) {
+            case 2: hipLaunchKernelGGL(dp_survtest_kernel<2>, gt, dim3(TEST_TILE), 0, s, a); break;
+            case 4: hipLaunchKernelGGL(dp_survtest_kernel<4>, gt, dim3(TEST_TILE), 0, s, a); break;
+            case 6: hipLaunchKernelGGL(dp_survtest_kernel<6>, gt, dim3(TEST_TILE), 0, s, a); break;
+            case 8: hipLaunchKernelGGL(dp_survtest_kernel<8>, gt, dim3(TEST_TILE), 0, s, a); break;
+            default: hipLaunchKernelGGL(dp_survtest_kernel<0>, gt, dim3(TEST_TILE), 0, s, a);
+        }
+        SATMI_HIP(hipEventRecord(ev[1], s));
+        hipLaunchKernelGGL(dp_kept_kernel, dim3(1), dim3(POP_THREADS), 0, s, a);
+        hipLaunchKernelGGL(dp_assemble_kernel, dim3(gc), dim3(64 * ASM_WAVES), 0, s, a);
         SATMI_HIP(hipGetLastError());
-        int32_t pop[3] = {0, 0, 0};
-        int32_t ovf = 0;
-        SATMI_HIP(hipMemcpyAsync(pop, misc.as<int32_t>() + 4, 12, hipMemcpyDeviceToHost, s));
-        SATMI_HIP(hipMemcpyAsync(&ovf, misc.p, 4, hipMemcpyDeviceToHost, s));
+        return SATMI_OK;
+    };
+    const bool record = h_rec_lits && h_rec_clause_off && h_rec_step_off;
+    int64_t rec_clauses = 0, rec_lits = 0;
+    int recorded_steps = 0;
+    std::vector<int64_t> h_off;
+    std::vector<int32_t> h_mask, h_arena;
+    int enqueued = 0;   // steps enqueued since the last resume
+    for (;;) {
+        // at most V steps eliminate a variable, then one pop finds the set empty
+        const int batch = record ? 1 : std::min(64, V + 1);
+        for (int k = 0; k < batch; ++k) DP_TRY(enqueue_step(A));
+        enqueued += batch;
+        SATMI_HIP(hipMemcpyAsync(Wk.pin, Wk.state.p, sizeof(DpState), hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
-        if (ovf || pop[2]) {
+        if (st.set_ovf) {
             set_error("satmi_dp_host: set model table overflow");
             return SATMI_ERR_TOO_LARGE;
         }
-        if (pool_pending) {   // the previous step's exact pool size, copied behind its assembly
-            pool_cur = Wk.pin[0];
-            pool_pending = false;
-        }
-        if (pop[1] == 0) break;   // `while variables` ends: True (REF.py:130)
-        if (step_limit > 0 && steps >= step_limit) {
-            result = -1;
-            break;
-        }
-        if (time_limit_s > 0 &&
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > time_limit_s) {
-            result = -1;
-            break;
-        }
-        const int32_t var = pop[0];
-        const int d = var2dense[var];
-        if (h_trace_vars && steps < trace_cap) h_trace_vars[steps] = var;
-        ++steps;
-        // split (REF.py:106-108)
-        DP_TRY(fpos.need(8 * (size_t)ncl));
-        DP_TRY(fneg.need(8 * (size_t)ncl));
-        DP_TRY(frem.need(8 * (size_t)ncl));
-        unsigned long long *d_mx = (unsigned long long *)(misc.as<char>() + 48);
-        SATMI_HIP(hipMemsetAsync(d_mx, 0, 16, s));
-        hipLaunchKernelGGL(dp_split_kernel, dim3(grid_for(ncl)), dim3(PRIM_BLOCK), 0, s, Lc, ncl, W, d,
-                           fpos.as<int64_t>(), fneg.as<int64_t>(), frem.as<int64_t>(), d_mx);
-        // the three lists with one count read-back
-        DP_TRY(counts3.need(3 * sizeof(int64_t)));
-        int64_t *c3 = counts3.as<int64_t>();
-        DP_TRY(compact_deferred(fpos.as<int64_t>(), ncl, scanpos, tiles, c3 + 0, plist, s));
-        DP_TRY(compact_deferred(fneg.as<int64_t>(), ncl, scanpos, tiles, c3 + 1, nlist, s));
-        DP_TRY(compact_deferred(frem.as<int64_t>(), ncl, scanpos, tiles, c3 + 2, rlist, s));
-        int64_t h3[3] = {0, 0, 0};
-        unsigned long long mx[2] = {0, 0};
-        SATMI_HIP(hipMemcpyAsync(h3, c3, sizeof(h3), hipMemcpyDeviceToHost, s));
-        SATMI_HIP(hipMemcpyAsync(mx, d_mx, sizeof(mx), hipMemcpyDeviceToHost, s));
-        SATMI_HIP(hipStreamSynchronize(s));
-        const int64_t np = h3[0], nn = h3[1], nr = h3[2];
-        const int64_t npairs = np * nn;
-        // resolvent bitsets + flags (REF.py:111-119)
-        int64_t m = 0;
-        unsigned long long first_empty = ~0ull;
-        if (npairs > 0) {
-            DP_TRY(rbits.need(8 * (size_t)npairs * K));
-            DP_TRY(nontaut.need(8 * (size_t)npairs));
-            SATMI_HIP(hipMemsetAsync(misc.as<char>() + 32, 0xff, 8, s));
-            hipLaunchKernelGGL(dp_pairs_kernel, dim3(grid_for(npairs)), dim3(PRIM_BLOCK), 0, s, Lc,
-                               plist.as<int64_t>(), nlist.as<int64_t>(), nn, npairs, W, d, rbits.as<uint64_t>(),
-                               nontaut.as<int64_t>(), (unsigned long long *)(misc.as<char>() + 32));
-            SATMI_HIP(hipGetLastError());
-            SATMI_HIP(hipMemcpyAsync(&first_empty, misc.as<char>() + 32, 8, hipMemcpyDeviceToHost, s));
-            DP_TRY(compact(nontaut.as<int64_t>(), npairs, scanpos, tiles, grand, ntlist, &m, s));
-        }
-        // the reference stops at the first empty resolvent, or (clause_limit) when
-        // remaining + new grows past the limit, whichever comes first in pair order
-        int64_t limit_pair = -1;
-        const int64_t kth = std::max<int64_t>(clause_limit - nr, 0);   // 0-based index of the offending new clause
-        if (clause_limit > 0 && m > kth) {
-            int64_t p = 0;
-            SATMI_HIP(hipMemcpyAsync(&p, ntlist.as<int64_t>() + kth, 8, hipMemcpyDeviceToHost, s));
-            SATMI_HIP(hipStreamSynchronize(s));
-            limit_pair = p;
-        }
-        if (first_empty != ~0ull && (limit_pair < 0 || (int64_t)first_empty <= limit_pair)) {
-            result = 0;   // empty clause: unsatisfiable (REF.py:117-118)
-            break;
-        }
-        if (limit_pair >= 0) {
-            result = -1;
-            break;
-        }
-        // unique_new (REF.py:122-125)
-        int64_t nkept = 0;
-        if (m > 0) {
-            DP_TRY(kept.need(8 * (size_t)m));
-            const int64_t *rl = rlist.as<int64_t>(), *ntl = ntlist.as<int64_t>();
-            const uint64_t *rb = rbits.as<uint64_t>();
-            int64_t *kp = kept.as<int64_t>();
-            unsigned long long *tc = (unsigned long long *)(misc.as<char>() + 40);
-            hipEvent_t *ev_sub = next_events();
-            if (!ev_sub) {
-                set_error("satmi_dp_host: hipEventCreate failed");
-                return SATMI_ERR_HIP;
+        if (st.overflow) {   // grow what ran out, then run the step again
+            const int cur = st.cur;
+            if (st.overflow & OVF_PAIRS) DP_TRY(grow_pairs(Wk, st.need[0], K));
+            if (st.overflow & OVF_NCL) DP_TRY(grow_ncl(Wk, st.need[1], K, cur, st.ncl));
+            if (st.overflow & OVF_ARENA) {
+                DP_TRY(Wk.arena.need(4 * (size_t)st.need[2], s, 4 * (size_t)st.arena_top));
+                Wk.arena_cap = (int64_t)(Wk.arena.cap / 4);
             }
-            SATMI_HIP(hipEventRecord(ev_sub[0], s));
-            if (K <= 8 && (K & 1) == 0) {
-                auto tiled = [&](const int64_t *sel, int64_t nsel, int64_t lo, int64_t hi) {
-                    const dim3 g((unsigned)((nsel + SUB_TILE - 1) / SUB_TILE),
-                                 (unsigned)std::max<int64_t>(1, (hi - lo + SUB_CHUNK - 1) / SUB_CHUNK));
-                    if (K == 2)
-                        hipLaunchKernelGGL((dp_subsume_tiled_kernel<2>), g, dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl,
-                                           sel, nsel, lo, hi, kp, tc);
-                    else if (K == 4)
-                        hipLaunchKernelGGL((dp_subsume_tiled_kernel<4>), g, dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl,
-                                           sel, nsel, lo, hi, kp, tc);
-                    else if (K == 6)
-                        hipLaunchKernelGGL((dp_subsume_tiled_kernel<6>), g, dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl,
-                                           sel, nsel, lo, hi, kp, tc);
-                    else
-                        hipLaunchKernelGGL((dp_subsume_tiled_kernel<8>), g, dim3(SUB_TILE), 0, s, Lc, rl, nr, rb, ntl,
-                                           sel, nsel, lo, hi, kp, tc);
-                };
-                hipLaunchKernelGGL(dp_ones_kernel, dim3(grid_for(m)), dim3(PRIM_BLOCK), 0, s, kp, m);
-                const int64_t total = nr + m;
-                const int64_t pre = std::min<int64_t>(SUB_PREFIX, total);
-                tiled(nullptr, m, 0, pre);   // every new clause: the first candidates
-                if (pre < total) {           // survivors: the rest
-                    int64_t nsurv = 0;
-                    DP_TRY(compact(kp, m, kpos, tiles, grand, klist, &nsurv, s));
-                    if (nsurv > 0) tiled(klist.as<int64_t>(), nsurv, pre, total);
-                }
-            } else {
-                hipLaunchKernelGGL(dp_subsume_kernel, dim3(grid_for(m * 64)), dim3(PRIM_BLOCK), 0, s, Lc, rl, nr, rb,
-                                   ntl, m, K, kp);
+            if (st.overflow & OVF_XS) {
+                DP_TRY(Wk.xs.need(4 * (size_t)st.need[3], s));
+                Wk.xs_cap = (int64_t)(Wk.xs.cap / 4);
             }
-            SATMI_HIP(hipEventRecord(ev_sub[1], s));
+            st.overflow = 0;
+            st.done = 0;
+            SATMI_HIP(hipMemcpyAsync(Wk.state.p, Wk.pin, sizeof(DpState), hipMemcpyHostToDevice, s));
+            A = args();
+            SATMI_HIP(hipMemsetAsync(Wk.firstpos.p, 0xFF, 8 * (size_t)V, s));
+            hipLaunchKernelGGL(dp_firstpos_kernel, dim3(grid_for(std::max<int64_t>(st.ncl, 1))), dim3(256), 0, s, A);
             SATMI_HIP(hipGetLastError());
-            g_dp_stats.new_clauses += m;
-            g_dp_stats.candidates_bytes += (nr + m) * K * 8;
-            DP_TRY(compact(kept.as<int64_t>(), m, kpos, tiles, grand, klist, &nkept, s));
+            enqueued = 0;
+            continue;
         }
-        if (nkept > 0) {
-            // images of AX, BY and the kept resolvents (capacities from the split's mx)
-            DP_TRY(A.reserve(np, cap_for((int64_t)mx[0])));
-            DP_TRY(B.reserve(nn, cap_for((int64_t)mx[1])));
-            DP_TRY(R.reserve(nkept, cap_for((int64_t)mx[0] + (int64_t)mx[1])));
-            hipLaunchKernelGGL(dp_diff_kernel, dim3(grid_for(np)), dim3(PRIM_BLOCK), 0, s, Lc, plist.as<int64_t>(),
-                               np, var, A.view(), misc.as<int>());
-            hipLaunchKernelGGL(dp_diff_kernel, dim3(grid_for(nn)), dim3(PRIM_BLOCK), 0, s, Lc, nlist.as<int64_t>(),
-                               nn, -var, B.view(), misc.as<int>());
-            hipLaunchKernelGGL(dp_build_kernel, dim3(grid_for(m)), dim3(PRIM_BLOCK), 0, s, A.view(), B.view(),
-                               ntlist.as<int64_t>(), kept.as<int64_t>(), kpos.as<int64_t>(), m, nn, R.view(),
-                               misc.as<int>());
-            SATMI_HIP(hipGetLastError());
-        }
-        // clauses = remaining_clauses + unique_new (REF.py:127)
-        const int64_t ncl2 = nr + nkept;
-        int64_t pool2 = 0;
-        if (ncl2 > 0) {
-            DP_TRY(sizes.need(8 * (size_t)ncl2));
-            DP_TRY(offs.need(8 * (size_t)ncl2));
-            hipLaunchKernelGGL(dp_sizes_kernel, dim3(grid_for(ncl2)), dim3(PRIM_BLOCK), 0, s, Lc, rlist.as<int64_t>(),
-                               nr, R.view(), nkept, sizes.as<int64_t>());
-            DP_TRY(tiles.need(8 * (size_t)((ncl2 + SCAN_TILE - 1) / SCAN_TILE + 1)));
-            DP_TRY(exclusive_scan(sizes.as<int64_t>(), offs.as<int64_t>(), ncl2, tiles.as<int64_t>(),
-                                  grand.as<int64_t>(), s));
-            // the next generation's pool: reserved for a bound (the remaining
-            // clauses' tables are regions of g[cur]'s pool; a kept resolvent's
-            // image has <= 2 x R.cap slots), the exact size copied back behind
-            // the assembly and read after the next step's first wait (no wait
-            // here; recording reads it at once)
-            const int64_t pool_ub = pool_cur + nkept * 2 * R.cap;
-            SATMI_HIP(hipMemcpyAsync(Wk.pin, grand.p, 8, hipMemcpyDeviceToHost, s));
-            const int nxt = cur ^ 1;
-            DP_TRY(g[nxt].reserve(ncl2, K, pool_ub));
-            hipLaunchKernelGGL(dp_assemble_kernel, dim3(grid_for(ncl2)), dim3(PRIM_BLOCK), 0, s, Lc,
-                               rlist.as<int64_t>(), nr, R.view(), klist.as<int64_t>(), nkept, rbits.as<uint64_t>(),
-                               ntlist.as<int64_t>(), offs.as<int64_t>(), K, g[nxt].view());
-            SATMI_HIP(hipGetLastError());
-            cur = nxt;
-            pool_cur = pool_ub;
-            pool_pending = true;
-        }
-        ncl = ncl2;
-        // record the clause list after the step, each clause in its set iteration order
-        if (h_rec_lits && h_rec_clause_off && h_rec_step_off && steps < rec_step_cap) {
-            h_off.resize((size_t)std::max<int64_t>(ncl, 1));
-            h_mask.resize((size_t)std::max<int64_t>(ncl, 1));
-            h_pool.resize((size_t)std::max<int64_t>(pool2, 1));
-            if (ncl > 0) {
-                SATMI_HIP(hipStreamSynchronize(s));   // Wk.pin[0] = pool2
-                pool2 = Wk.pin[0];
-                h_pool.resize((size_t)std::max<int64_t>(pool2, 1));
-                SATMI_HIP(hipMemcpyAsync(h_off.data(), g[cur].off.p, 8 * (size_t)ncl, hipMemcpyDeviceToHost, s));
-                SATMI_HIP(hipMemcpyAsync(h_mask.data(), g[cur].mask.p, 4 * (size_t)ncl, hipMemcpyDeviceToHost, s));
-                SATMI_HIP(hipMemcpyAsync(h_pool.data(), g[cur].pool.p, 4 * (size_t)pool2, hipMemcpyDeviceToHost, s));
+        if (record && st.pending && st.steps > recorded_steps && st.steps < rec_step_cap) {
+            // the clause list after this step, each clause in its set iteration order
+            const int64_t n2 = st.ncl2;
+            const int nxt = st.cur ^ 1;
+            h_off.resize((size_t)std::max<int64_t>(n2, 1));
+            h_mask.resize((size_t)std::max<int64_t>(n2, 1));
+            h_arena.resize((size_t)std::max<int64_t>(st.arena_top, 1));
+            if (n2 > 0) {
+                SATMI_HIP(hipMemcpyAsync(h_off.data(), Wk.g[nxt].off.p, 8 * (size_t)n2, hipMemcpyDeviceToHost, s));
+                SATMI_HIP(hipMemcpyAsync(h_mask.data(), Wk.g[nxt].mask.p, 4 * (size_t)n2, hipMemcpyDeviceToHost, s));
+                SATMI_HIP(hipMemcpyAsync(h_arena.data(), Wk.arena.p, 4 * (size_t)st.arena_top, hipMemcpyDeviceToHost,
+                                         s));
                 SATMI_HIP(hipStreamSynchronize(s));
             }
-            for (int64_t c = 0; c < ncl && rec_clauses + 1 < rec_clause_cap; ++c) {
+            for (int64_t c = 0; c < n2 && rec_clauses + 1 < rec_clause_cap; ++c) {
                 for (int64_t i = 0; i <= h_mask[c]; ++i) {
-                    const int32_t k = h_pool[h_off[c] + i];
+                    const int32_t k = h_arena[h_off[c] + i];
                     if (k != PY_EMPTY && k != PY_DUMMY && rec_lits < rec_lit_cap) h_rec_lits[rec_lits++] = k;
                 }
                 h_rec_clause_off[++rec_clauses] = rec_lits;
             }
-            h_rec_step_off[steps] = rec_clauses;
+            h_rec_step_off[st.steps] = rec_clauses;
+            recorded_steps = st.steps;
         }
-        // the set-model overflow flag (misc[0]) of this step is read with the
-        // next step's pop, or after the loop
+        if (st.done) break;
+        if (enqueued > V + 1) {   // cannot happen: every step eliminates a variable
+            set_error("satmi_dp_host: elimination did not terminate");
+            return SATMI_ERR_HIP;
+        }
     }
-    {
-        int32_t ovf2 = 0;
-        SATMI_HIP(hipMemcpyAsync(&ovf2, misc.p, 4, hipMemcpyDeviceToHost, s));
+    Wk.epoch = st.epoch + 1;
+    const int steps = st.steps;
+    if (h_trace_vars && steps > 0) {
+        std::vector<int32_t> tr((size_t)steps);
+        SATMI_HIP(hipMemcpyAsync(tr.data(), Wk.trace.p, 4 * (size_t)steps, hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
-        if (ovf2) {
-            set_error("satmi_dp_host: set model table overflow");
-            return SATMI_ERR_TOO_LARGE;
-        }
+        for (int k = 0; k < steps && k < trace_cap; ++k) h_trace_vars[k] = tr[(size_t)k];
     }
-    {
-        unsigned long long tests = 0;
-        SATMI_HIP(hipMemcpyAsync(&tests, misc.as<char>() + 40, 8, hipMemcpyDeviceToHost, s));
-        SATMI_HIP(hipStreamSynchronize(s));
-        g_dp_stats.tests = (int64_t)tests;
-        g_dp_stats.steps = steps;
-        for (size_t i = 0; i < nev; ++i) {   // the stream has drained
-            float ms = 0.0f;
-            if (hipEventElapsedTime(&ms, Wk.ev[2 * i], Wk.ev[2 * i + 1]) == hipSuccess) g_dp_stats.subsume_ms += ms;
-        }
+    g_dp_stats.steps = steps;
+    g_dp_stats.tests = st.tests;
+    g_dp_stats.new_clauses = st.new_total;
+    for (size_t i = 0; i < nev; ++i) {   // the stream has drained
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, Wk.ev[2 * i], Wk.ev[2 * i + 1]) == hipSuccess) g_dp_stats.subsume_ms += ms;
     }
-    *h_result = result;
+    *h_result = st.result;
     *h_steps = steps;
+    lease.ok = true;
     return SATMI_OK;
 }
 
@@ -895,5 +1323,21 @@ extern "C" int satmi_dp_last_stats(int64_t *steps, int64_t *subset_tests, int64_
     if (candidate_bytes) *candidate_bytes = g_dp_stats.candidates_bytes;
     if (words) *words = g_dp_stats.words;
     if (subsume_ms) *subsume_ms = g_dp_stats.subsume_ms;
+    return SATMI_OK;
+}
+
+// Free every idle workspace of this solver (device buffers, streams, pinned
+// words); calls in flight keep theirs.  The next call allocates afresh.
+extern "C" int satmi_dp_trim(void) {
+    std::vector<DpWork *> idle;
+    {
+        auto &P = dp_pool();
+        std::lock_guard<std::mutex> g(P.mu);
+        idle.swap(P.free_list);
+    }
+    for (DpWork *w : idle) {
+        (void)hipStreamSynchronize(w->stream);
+        delete w;
+    }
     return SATMI_OK;
 }

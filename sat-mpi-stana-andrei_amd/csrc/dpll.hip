@@ -1358,6 +1358,7 @@ extern "C" int satmi_dpll_batch_device(int num_instances, const int32_t *d_inst_
     uint32_t *wc = nullptr;
     int rc = device_work((hipStream_t)stream, &w, &wc);
     if (rc) return rc;
+    split_mark_unsplit((hipStream_t)stream);   // this launch does not split: its stats are all zero
     if (wide) {
         // one-wave workgroups, each with an HBM arena; resident waves bounded by
         // 32 per CU and by half the free device memory

@@ -32,7 +32,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -289,6 +291,221 @@ __global__ void res_append_kernel(const uint64_t *cand, const int64_t *flag, con
     }
 }
 
+// ---- packed keys (at most 31 variables): one fused pass.  Every clause is
+// one word P | N << 32, the dedup table holds the keys themselves and lives
+// for the whole saturation (it IS the reference's `seen`, REF.py:65/94), so a
+// pair's resolvent is classified and claimed in registers: no candidate
+// buffer, no flags, no compaction.  A claim (the key was absent) appends the
+// key after the clause list -- the pass's new-clause set is exactly the keys
+// claimed, whatever the order the hardware claims them in.  A pass's sizes live
+// on the device (ResState); the host enqueues passes without waiting.
+struct ResState {
+    int64_t ncl, jlo;             // clauses; first clause added by the previous pass
+    unsigned long long count;     // claims of the running pass (starts at slot_base)
+    int64_t passes;
+    int64_t pairs, candidates;    // whole saturation
+    uint64_t t0;                  // s_memrealtime at the start
+    int32_t done, result, empty, timeout, overflow, pad;
+};
+
+struct ResArgs {
+    ResState *st;
+    uint64_t *keys;      // packed clause keys, clause c at keys[c]
+    int64_t key_cap;
+    uint64_t *table;     // HT_EMPTY or a key, in buckets of RES_BUCKET slots
+    uint64_t tmask;      // bucket mask
+    int64_t *pass_new;   // device copy of the per-pass counts
+    int pass_cap;
+    int64_t max_passes, clause_limit;
+    uint64_t limit_ticks;
+    int64_t slot_base;   // test knob (satmi_resolution_debug_slot_base)
+};
+
+constexpr int RES_PROBE_MAX = 1 << 12;   // buckets: a probe run this long means the table is too full
+constexpr int RES_BUCKET = 8;             // slots per bucket: one 64-B read checks them all
+
+__global__ void __launch_bounds__(256) res_pack_kernel(const uint64_t *k2, int64_t n, uint64_t *keys, ResState *S) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) S->t0 = __builtin_amdgcn_s_memrealtime();
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
+        keys[c] = pack_key(k2 + 2 * c);
+}
+
+// Claim key r in a bucketed linear-probing table (slot order: bucket b's 8
+// slots, then bucket b+1's, ...; a key sits before the first empty slot of
+// its sequence).  1 = r was absent and this call inserted it, 0 = present,
+// -1 = the probe run exceeded RES_PROBE_MAX buckets.  The bucket is read with
+// plain loads: a slot only ever changes from HT_EMPTY to a key, so a stale
+// EMPTY is settled by the CAS and a key read is never wrong.
+__device__ __forceinline__ int bucket_claim(uint64_t *table, uint64_t bmask, uint64_t r) {
+    uint64_t b = (mix64(r) >> 3) & bmask;
+    for (int probes = 0; probes < RES_PROBE_MAX; ++probes) {
+        uint64_t *bk = table + b * RES_BUCKET;
+        const ulonglong2 *v = (const ulonglong2 *)bk;
+        const ulonglong2 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
+        const uint64_t sl[RES_BUCKET] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+        uint32_t empty = 0;
+#pragma unroll
+        for (int k = 0; k < RES_BUCKET; ++k) {
+            if (sl[k] == r) return 0;
+            empty |= (sl[k] == HT_EMPTY ? 1u : 0u) << k;
+        }
+        while (empty) {   // claim the first slot that is really empty, in slot order
+            const int k = __builtin_ctz(empty);
+            empty &= empty - 1;
+            const uint64_t cur =
+                atomicCAS((unsigned long long *)(bk + k), (unsigned long long)HT_EMPTY, (unsigned long long)r);
+            if (cur == HT_EMPTY) return 1;
+            if (cur == r) return 0;
+        }
+        b = (b + 1) & bmask;
+    }
+    return -1;
+}
+
+// keys [c0, c1) into the table (an input clause equal to an earlier one stays out)
+__global__ void __launch_bounds__(256) res_seed_kernel(uint64_t *table, uint64_t bmask, const uint64_t *keys,
+                                                       int64_t c0, int64_t c1, ResState *S) {
+    for (int64_t c = c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < c1; c += (int64_t)gridDim.x * blockDim.x)
+        if (bucket_claim(table, bmask, keys[c]) < 0) S->overflow = 1;
+}
+
+// One pass (REF.py:67-95): the pairs (i < j), j in [jlo, ncl), numbered
+// g = j(j-1)/2 + i, one pair per thread (grid-stride rounds): the lanes of a
+// wave share j (one broadcast key load) and read consecutive keys i, and no
+// thread walks a serial chain of probes.  A block's new keys collect in an LDS
+// buffer and are appended with ONE atomic on the pass's counter per flush (a
+// single global counter serialises: one atomic per wavefront with a claim was
+// the kernel's bound).
+constexpr int RES_ABUF = 2048;
+__global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
+    __shared__ uint64_t abuf[RES_ABUF];
+    __shared__ int wsum[4];
+    __shared__ int sh_stop, an;
+    __shared__ unsigned long long abase;
+    ResState *S = A.st;
+    if (S->done) return;
+    const int64_t jlo = S->jlo, ncl = S->ncl;
+    const uint64_t t0 = S->t0;
+    const int ln = lane_id(), tid = threadIdx.x;
+    const int64_t g0 = jlo * (jlo - 1) / 2, T = ncl * (ncl - 1) / 2 - g0;   // this pass's pairs
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int cand = 0;
+    if (tid == 0) an = 0;
+    // flush the buffered keys (block-uniform call)
+    const auto flush = [&]() {
+        const int na = min(an, RES_ABUF);
+        if (tid == 0 && na) abase = atomicAdd(&S->count, (unsigned long long)na);
+        __syncthreads();
+        const int64_t first = (int64_t)(abase - (unsigned long long)A.slot_base);
+        for (int t = tid; t < na; t += 256) {
+            if (ncl + first + t < A.key_cap)
+                A.keys[ncl + first + t] = abuf[t];
+            else
+                __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (tid == 0) an = 0;
+    };
+    int round = 0;
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < T; b0 += stride, ++round) {   // block-uniform
+        if ((round & 15) == 0) {
+            if (tid == 0) {
+                int stop = __hip_atomic_load(&S->empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                           __hip_atomic_load(&S->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!stop && A.limit_ticks && __builtin_amdgcn_s_memrealtime() - t0 > A.limit_ticks) {
+                    __hip_atomic_store(&S->timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = 1;
+                }
+                sh_stop = stop;
+            }
+            __syncthreads();
+            if (sh_stop) break;
+        }
+        const int64_t t = b0 + tid;
+        bool win = false;
+        uint64_t r = 0;
+        if (t < T) {
+            const int64_t g = g0 + t;
+            int64_t j = (int64_t)(0.5 + sqrt(0.25 + 2.0 * (double)g));   // j(j-1)/2 <= g < j(j+1)/2
+            while (j * (j - 1) / 2 > g) --j;
+            while (j * (j + 1) / 2 <= g) ++j;
+            const int64_t i = g - j * (j - 1) / 2;
+            const uint64_t a = A.keys[i], b = A.keys[j];
+            const uint32_t Pa = (uint32_t)a, Na = (uint32_t)(a >> 32), Pb = (uint32_t)b, Nb = (uint32_t)(b >> 32);
+            const uint32_t clash = (Pa & Nb) | (Na & Pb);
+            // exactly one clashing variable: the resolvent (two or more make
+            // every resolvent a tautology, REF.py:81)
+            if (clash && !(clash & (clash - 1))) {
+                const uint32_t P = (Pa | Pb) & ~clash, N = (Na | Nb) & ~clash;
+                if (!(P & N)) {
+                    if (!(P | N)) {
+                        __hip_atomic_store(&S->empty, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // REF.py:84-85
+                    } else {
+                        ++cand;
+                        r = (uint64_t)P | ((uint64_t)N << 32);
+                        const int c = bucket_claim(A.table, A.tmask, r);
+                        win = c > 0;
+                        if (c < 0) __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+        }
+        const uint64_t m = __ballot(win);
+        if (m) {   // clauses.extend(new), staged in the block's LDS buffer
+            int pos = 0;
+            if (ln == 0) pos = atomicAdd(&an, __popcll(m));
+            pos = __shfl(pos, 0) + __popcll(m & lanemask_lt());
+            if (win) abuf[pos] = r;   // room: flushed below before it can fill
+        }
+        __syncthreads();
+        if (an > RES_ABUF - 256) flush();   // block-uniform: an settled by the barrier
+    }
+    __syncthreads();
+    flush();
+    int tot;
+    {   // block sum of the candidates (every thread reaches here)
+        const int wid = tid >> 6;
+        const int incl = wave_incl_scan(cand);
+        if (ln == 63) wsum[wid] = incl;
+        __syncthreads();
+        tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    }
+    if (tid == 0 && tot) atomicAdd((unsigned long long *)&S->candidates, (unsigned long long)tot);
+}
+
+// after a pass (one thread): the verdict or the next pass's bounds
+__global__ void res_finish_pass_kernel(ResArgs A) {
+    ResState *S = A.st;
+    if (S->done) return;
+    if (S->overflow) {   // the host grows the buffers and runs this pass again
+        S->done = 1;
+        return;
+    }
+    const int64_t nnew = (int64_t)(S->count - (unsigned long long)A.slot_base);
+    S->pairs += (S->ncl * (S->ncl - 1) - S->jlo * (S->jlo - 1)) / 2;
+    if (S->empty) {   // an empty resolvent: unsatisfiable (REF.py:84-85)
+        S->result = 0;
+        S->done = 1;
+        return;
+    }
+    if (S->timeout) {   // the deadline ended the pass early (REF.py:417-437)
+        S->done = 1;
+        return;
+    }
+    if (nnew == 0) {   // no new clauses can be derived (REF.py:91-92)
+        S->result = 1;
+        S->done = 1;
+        return;
+    }
+    if (S->passes < A.pass_cap) A.pass_new[S->passes] = nnew;
+    S->passes += 1;
+    S->jlo = S->ncl;
+    S->ncl += nnew;
+    S->count = (unsigned long long)A.slot_base;
+    if ((A.max_passes > 0 && S->passes >= A.max_passes) || (A.clause_limit > 0 && S->ncl > A.clause_limit))
+        S->done = 1;   // result stays -1
+}
+
 // ------------------------------------------------------------------ host side
 namespace {
 
@@ -341,7 +558,8 @@ uint64_t table_slots(int64_t keys) {
 constexpr int64_t PAIR_CHUNK = 1ll << 27;
 constexpr size_t CAND_BYTES = (size_t)1 << 30;
 
-int64_t g_slot_base = 0;   // test knob: first append slot of the pair kernel
+int64_t g_slot_base = 0;            // test knob: first append slot of the pair kernel
+size_t g_cand_bytes = CAND_BYTES;   // test knob: the candidate buffer's cap (forces the re-run path)
 
 // Work and kernel time of the last satmi_resolution_host call (HIP events on
 // its stream around the pair and claim launches): bench.py's roofline input.
@@ -382,31 +600,253 @@ struct EventTimer {
     }
 };
 
-// Device buffers of satmi_resolution_host, kept between calls (grow-only) per
-// host thread and device, with the thread's own non-blocking stream: a
-// saturation of a small formula is a few passes of small launches, so
-// allocating its buffers per call cost more than its kernels, and calls from
-// several threads overlap.  Never destroyed (no hipFree after the runtime's
-// teardown).
+// Device buffers of satmi_resolution_host, kept between calls (grow-only) in a
+// process-wide pool: a call takes a free workspace of its device (or makes
+// one) and returns it when done, so concurrent calls from any number of host
+// threads each own one, overlap on the device (each its own non-blocking
+// stream), and the number of workspaces is the peak number of concurrent
+// calls.  A saturation of a small formula is a few passes of small launches,
+// so allocating its buffers per call cost more than its kernels.
 struct ResWork {
     DevBuf d_off, d_lits, d_map, clauses, cand, counters, table, flag, pos, slotv, tiles, grand;
+    DevBuf keys, state, passnew;   // the packed path
     EventTimer t_pairs, t_claims;
     hipStream_t stream = nullptr;
     unsigned long long *pin = nullptr;   // pinned host words: the per-chunk counters and claim count
-};
-ResWork *res_work(int dev) {
-    thread_local std::vector<ResWork *> mine;
-    if ((int)mine.size() <= dev) mine.resize(dev + 1, nullptr);
-    if (!mine[dev]) {
-        ResWork *w = new ResWork;
-        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
-            hipHostMalloc((void **)&w->pin, 64, hipHostMallocDefault) != hipSuccess) {
-            delete w;
-            return nullptr;
-        }
-        mine[dev] = w;
+    ResState *pst = nullptr;             // pinned host copy of the packed path's state
+    int dev = 0;
+    ~ResWork() {   // only a workspace that failed part-way is destroyed (after its stream drained)
+        if (stream) (void)hipStreamDestroy(stream);
+        if (pin) (void)hipHostFree(pin);
+        if (pst) (void)hipHostFree(pst);
     }
-    return mine[dev];
+};
+
+struct ResPool {
+    std::mutex mu;
+    std::vector<ResWork *> free_list;
+};
+ResPool &res_pool() {
+    static ResPool *p = new ResPool;   // never destroyed: no hipFree after the runtime's teardown
+    return *p;
+}
+ResWork *res_acquire(int dev) {
+    ResPool &P = res_pool();
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        for (size_t i = 0; i < P.free_list.size(); ++i)
+            if (P.free_list[i]->dev == dev) {
+                ResWork *w = P.free_list[i];
+                P.free_list.erase(P.free_list.begin() + (long)i);
+                return w;
+            }
+    }
+    ResWork *w = new ResWork;
+    w->dev = dev;
+    if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&w->pin, 64, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&w->pst, sizeof(ResState), hipHostMallocDefault) != hipSuccess) {
+        delete w;
+        return nullptr;
+    }
+    return w;
+}
+// A call's hold on a workspace: back to the pool after a call that completed,
+// destroyed after one that failed part-way (its table may hold stale keys).
+struct ResLease {
+    ResWork *w;
+    bool ok = false;
+    ~ResLease() {
+        if (!w) return;
+        if (ok) {
+            ResPool &P = res_pool();
+            std::lock_guard<std::mutex> g(P.mu);
+            P.free_list.push_back(w);
+        } else {
+            (void)hipStreamSynchronize(w->stream);
+            delete w;
+        }
+    }
+};
+
+// decode a pass's new keys (packed or bitset words) into sorted literal lists
+void record_pass(const std::vector<uint64_t> &hkeys, int64_t nnew, bool packed, int W, int V,
+                 const std::vector<int32_t> &dense2var, int passes, int32_t *h_rec_lits, int64_t rec_lit_cap,
+                 int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_pass_off, int64_t &rec_clauses,
+                 int64_t &rec_lits) {
+    // each clause as ascending literals, the clauses in ascending order
+    // (deterministic whatever the append order)
+    std::vector<std::vector<int32_t>> pass((size_t)nnew);
+    for (int64_t c = 0; c < nnew; ++c) {
+        for (int d = 0; d < V; ++d) {
+            bool pos, neg;
+            if (packed) {
+                const uint64_t k = hkeys[(size_t)c];
+                pos = (k >> d) & 1ull;
+                neg = (k >> (32 + d)) & 1ull;
+            } else {
+                const uint64_t *k = hkeys.data() + c * 2 * W;
+                pos = (k[d >> 6] >> (d & 63)) & 1ull;
+                neg = (k[W + (d >> 6)] >> (d & 63)) & 1ull;
+            }
+            if (pos) pass[(size_t)c].push_back(dense2var[(size_t)d]);
+            if (neg) pass[(size_t)c].push_back(-dense2var[(size_t)d]);
+        }
+        std::sort(pass[(size_t)c].begin(), pass[(size_t)c].end());
+    }
+    std::sort(pass.begin(), pass.end());
+    for (const auto &cl : pass) {
+        if (rec_clauses + 1 >= rec_clause_cap || rec_lits + (int64_t)cl.size() > rec_lit_cap) break;
+        std::copy(cl.begin(), cl.end(), h_rec_lits + rec_lits);
+        rec_lits += (int64_t)cl.size();
+        h_rec_clause_off[++rec_clauses] = rec_lits;
+    }
+    h_rec_pass_off[passes + 1] = rec_clauses;
+}
+
+
+// grow the packed key buffer to >= want keys, keeping keys [0, keep)
+int grow_keys(ResWork &wk, int64_t want, int64_t keep, hipStream_t s) {
+    if ((size_t)want * 8 <= wk.keys.cap) return SATMI_OK;
+    DevBuf grown;
+    SATMI_TRY(grown.reserve(8 * (size_t)want));
+    if (keep > 0) SATMI_HIP(hipMemcpyAsync(grown.p, wk.keys.p, 8 * (size_t)keep, hipMemcpyDeviceToDevice, s));
+    std::swap(grown.p, wk.keys.p);
+    std::swap(grown.cap, wk.keys.cap);
+    SATMI_HIP(hipStreamSynchronize(s));   // before `grown` frees the old buffer
+    return SATMI_OK;
+}
+
+// The packed path (<= 31 variables): the clause keys, the table and the state
+// stay on the device for the whole saturation; passes are enqueued in batches
+// and the host waits once per batch (once per pass when recording).  A pass
+// that ran out of key or table room is re-run after the host grows them.
+int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t clause_limit, double time_limit_s,
+                      int64_t slot_base, int V, const std::vector<int32_t> &dense2var, int32_t *h_result,
+                      int32_t *h_passes, int64_t *h_pass_new, int pass_cap, int32_t *h_rec_lits,
+                      int64_t rec_lit_cap, int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_pass_off,
+                      int rec_pass_cap) {
+    hipStream_t s = wk.stream;
+    const int PCAP = 1 << 12;   // passes whose counts the device keeps (the host copies out pass_cap of them)
+    SATMI_TRY(wk.keys.reserve(8 * (size_t)std::max<int64_t>(4 * (int64_t)nclauses, 1 << 14)));
+    SATMI_TRY(wk.state.reserve(sizeof(ResState)));
+    SATMI_TRY(wk.passnew.reserve(8 * (size_t)PCAP));
+    int64_t key_cap = (int64_t)(wk.keys.cap / 8);
+    // the table: a power of two >= 2x the keys it can hold (load <= 1/2; a
+    // table larger than needed only spreads the probes over more cache lines)
+    const auto slots_for = [](int64_t nkeys) {   // a power of two, >= 8 buckets
+        uint64_t c = 1 << 12;
+        while (c < 2 * (uint64_t)nkeys) c <<= 1;
+        return c;
+    };
+    uint64_t tslots = slots_for(key_cap);
+    SATMI_TRY(wk.table.reserve(8 * tslots));
+    if (nclauses > 0)
+        hipLaunchKernelGGL(res_pack_kernel, dim3(grid_for(nclauses)), dim3(256), 0, s, wk.clauses.as<uint64_t>(),
+                           (int64_t)nclauses, wk.keys.as<uint64_t>(), wk.state.as<ResState>());
+    ResState &st = *wk.pst;
+    st = ResState{};
+    st.ncl = nclauses;
+    st.count = (unsigned long long)slot_base;
+    st.result = -1;
+    // the deadline is measured on the device from the pack kernel's start (t0
+    // written by it): copy the state behind it without t0
+    const auto push_state = [&]() -> int {
+        SATMI_HIP(hipMemcpyAsync(wk.state.p, wk.pst, offsetof(ResState, t0), hipMemcpyHostToDevice, s));
+        SATMI_HIP(hipMemcpyAsync((char *)wk.state.p + offsetof(ResState, done), &wk.pst->done,
+                                 sizeof(ResState) - offsetof(ResState, done), hipMemcpyHostToDevice, s));
+        return SATMI_OK;
+    };
+    SATMI_TRY(push_state());   // (no clauses: no pairs, the deadline is never read)
+    const auto seed = [&](int64_t nkeys) -> int {   // a fresh table holding keys [0, nkeys)
+        SATMI_HIP(hipMemsetAsync(wk.table.p, 0xFF, 8 * tslots, s));   // HT_EMPTY
+        if (nkeys > 0)
+            hipLaunchKernelGGL(res_seed_kernel, dim3(grid_for(nkeys)), dim3(256), 0, s, wk.table.as<uint64_t>(),
+                               tslots / RES_BUCKET - 1, wk.keys.as<uint64_t>(), (int64_t)0, nkeys,
+                               wk.state.as<ResState>());
+        SATMI_HIP(hipGetLastError());
+        return SATMI_OK;
+    };
+    SATMI_TRY(seed(nclauses));
+    double hz = 1e8;
+    (void)satmi_wallclock_hz(&hz);
+    ResArgs A;
+    const auto args = [&]() {
+        A.st = wk.state.as<ResState>();
+        A.keys = wk.keys.as<uint64_t>();
+        A.key_cap = key_cap;
+        A.table = wk.table.as<uint64_t>();
+        A.tmask = tslots / RES_BUCKET - 1;   // bucket mask
+        A.pass_new = wk.passnew.as<int64_t>();
+        A.pass_cap = PCAP;
+        A.max_passes = max_passes;
+        A.clause_limit = clause_limit;
+        A.limit_ticks = time_limit_s > 0 ? (uint64_t)std::max(1.0, time_limit_s * hz) : 0;
+        A.slot_base = slot_base;
+    };
+    args();
+    EventTimer &t_pairs = wk.t_pairs;
+    t_pairs.reset();
+    g_stats = ResStats{};
+    const bool record = h_rec_lits && h_rec_clause_off && h_rec_pass_off;
+    int64_t rec_clauses = 0, rec_lits = 0;
+    std::vector<uint64_t> hkeys;
+    const dim3 pass_grid(4096);   // grid-stride rounds of 256 pairs per block
+    for (;;) {
+        // passes per wait: all of them when the count is bounded (<= 16)
+        const int64_t left = max_passes > 0 ? max_passes - st.passes : 4;
+        const int batch = record ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(left, 16));
+        const int64_t ncl_before = st.ncl;
+        for (int b = 0; b < batch; ++b) {
+            t_pairs.begin(s);
+            hipLaunchKernelGGL(res_pass_packed_kernel, pass_grid, dim3(256), 0, s, A);
+            t_pairs.end(s);
+            hipLaunchKernelGGL(res_finish_pass_kernel, dim3(1), dim3(1), 0, s, A);
+        }
+        SATMI_HIP(hipGetLastError());
+        SATMI_HIP(hipMemcpyAsync(wk.pst, wk.state.p, sizeof(ResState), hipMemcpyDeviceToHost, s));
+        SATMI_HIP(hipStreamSynchronize(s));
+        if (st.overflow) {   // grow the key buffer and / or the table, re-seed, run the pass again
+            // the claims of the stopped pass (all of its new keys when only
+            // the key buffer ran out) plus a quarter
+            const int64_t claims = (int64_t)(st.count - (unsigned long long)slot_base);
+            const int64_t want = std::max<int64_t>(key_cap + key_cap / 2, st.ncl + claims + claims / 4 + 1024);
+            SATMI_TRY(grow_keys(wk, want, st.ncl, s));
+            key_cap = (int64_t)(wk.keys.cap / 8);
+            tslots = slots_for(key_cap);
+            SATMI_TRY(wk.table.reserve(8 * tslots));
+            args();
+            st.overflow = 0;
+            st.done = 0;
+            st.empty = 0;
+            st.timeout = 0;
+            st.count = (unsigned long long)slot_base;
+            SATMI_HIP(hipMemcpyAsync(wk.state.p, wk.pst, sizeof(ResState), hipMemcpyHostToDevice, s));
+            SATMI_TRY(seed(st.ncl));   // (after the state: a seed overflow flag must survive)
+            continue;
+        }
+        if (record && st.passes > 0 && st.ncl > ncl_before && st.passes < rec_pass_cap) {
+            const int64_t nnew = st.ncl - ncl_before;   // batch == 1: this pass's additions
+            hkeys.resize((size_t)nnew);
+            SATMI_HIP(hipMemcpyAsync(hkeys.data(), wk.keys.as<uint64_t>() + ncl_before, 8 * (size_t)nnew,
+                                     hipMemcpyDeviceToHost, s));
+            SATMI_HIP(hipStreamSynchronize(s));
+            record_pass(hkeys, nnew, true, 1, V, dense2var, (int)st.passes - 1, h_rec_lits, rec_lit_cap,
+                        h_rec_clause_off, rec_clause_cap, h_rec_pass_off, rec_clauses, rec_lits);
+        }
+        if (st.done) break;
+    }
+    const int np = (int)std::min<int64_t>(st.passes, std::min(pass_cap, PCAP));
+    if (h_pass_new && np > 0)
+        SATMI_HIP(hipMemcpyAsync(h_pass_new, wk.passnew.p, 8 * (size_t)np, hipMemcpyDeviceToHost, s));
+    SATMI_HIP(hipStreamSynchronize(s));
+    *h_result = st.result;
+    *h_passes = (int32_t)st.passes;
+    g_stats.pairs = st.pairs;
+    g_stats.candidates = st.candidates;
+    g_stats.pair_ms = t_pairs.total();
+    g_stats.claim_ms = 0.0;   // fused into the pass kernel
+    return SATMI_OK;
 }
 
 }  // namespace
@@ -420,6 +860,15 @@ extern "C" int satmi_resolution_last_stats(int64_t *pairs, int64_t *candidates, 
     if (candidates) *candidates = g_stats.candidates;
     if (pair_ms) *pair_ms = g_stats.pair_ms;
     if (claim_ms) *claim_ms = g_stats.claim_ms;
+    return SATMI_OK;
+}
+
+extern "C" int satmi_resolution_debug_cand_bytes(int64_t bytes) {
+    if (bytes < 0) {
+        set_error("satmi_resolution_debug_cand_bytes: negative size");
+        return SATMI_ERR_ARG;
+    }
+    g_cand_bytes = bytes ? (size_t)bytes : CAND_BYTES;
     return SATMI_OK;
 }
 
@@ -454,8 +903,8 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
     const int64_t L = nclauses > 0 ? h_clause_off[nclauses] : 0;
     int maxvar = 0;
     for (int64_t i = 0; i < L; ++i) {
-        if (h_lits[i] == 0) {
-            set_error("satmi_resolution_host: literal 0");
+        if (h_lits[i] == 0 || h_lits[i] == INT32_MIN) {
+            set_error("satmi_resolution_host: literal 0 / INT32_MIN");
             return SATMI_ERR_ARG;
         }
         maxvar = std::max(maxvar, std::abs(h_lits[i]));
@@ -470,15 +919,16 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
     const int V = (int)dense2var.size();
     const int W = std::max(1, (V + 63) / 64);
     const int K = 2 * W;
-    const bool packed = V <= 31;   // the packed table (see pack_key)
+    const bool packed = V <= 31;   // the packed table (see pack_key) and the fused pass
     const int64_t slot_base = g_slot_base;
     int dev_id = 0;
     SATMI_HIP(hipGetDevice(&dev_id));
-    ResWork *wk = res_work(dev_id);
-    if (!wk) {
+    ResLease lease{res_acquire(dev_id)};
+    if (!lease.w) {
         set_error("satmi_resolution_host: hipStreamCreate failed");
         return SATMI_ERR_HIP;
     }
+    ResWork *wk = lease.w;
     hipStream_t s = wk->stream;
     DevBuf &d_off = wk->d_off, &d_lits = wk->d_lits, &d_map = wk->d_map, &clauses = wk->clauses, &cand = wk->cand,
            &counters = wk->counters;
@@ -496,6 +946,13 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
                            d_off.as<int32_t>(), d_lits.as<int32_t>(), d_map.as<int32_t>(), W,
                            clauses.as<uint64_t>());
         SATMI_HIP(hipGetLastError());
+    }
+    if (packed) {
+        const int rc = resolution_packed(*wk, nclauses, max_passes, clause_limit, time_limit_s, slot_base, V,
+                                         dense2var, h_result, h_passes, h_pass_new, pass_cap, h_rec_lits,
+                                         rec_lit_cap, h_rec_clause_off, rec_clause_cap, h_rec_pass_off, rec_pass_cap);
+        if (rc == SATMI_OK) lease.ok = true;
+        return rc;
     }
     DevBuf &table = wk->table, &flag = wk->flag, &pos = wk->pos, &slotv = wk->slotv, &tiles = wk->tiles,
            &grand = wk->grand;
@@ -578,7 +1035,7 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
             j1 = std::min(ncl, std::max(j1, j0 + 1));
             while (j1 > j0 + 1 && (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2 > PAIR_CHUNK) --j1;
             const int64_t npairs = std::max<int64_t>(1, (j1 * (j1 - 1) - j0 * (j0 - 1)) / 2);
-            SATMI_TRY(cand.reserve(std::min(8 * (size_t)npairs * K, std::max(CAND_BYTES, cand.cap))));
+            SATMI_TRY(cand.reserve(std::min(8 * (size_t)npairs * K, std::max(g_cand_bytes, cand.cap))));
             struct {
                 unsigned long long count;
                 int empty;
@@ -597,7 +1054,11 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
                 SATMI_HIP(hipStreamSynchronize(s));
                 std::memcpy(&hc, wk->pin, 16);
                 const int64_t counted = (int64_t)(hc.count - (unsigned long long)slot_base);
-                if (hc.empty || counted <= cap || attempt > 0) break;
+                if (hc.empty || counted <= cap) break;
+                if (attempt > 0) {   // cannot happen: the re-run had room for every counted candidate
+                    set_error("satmi_resolution_host: candidate buffer overflow after a re-run");
+                    return SATMI_ERR_HIP;
+                }
                 SATMI_TRY(cand.reserve(8 * (size_t)counted * K));   // overflowed: re-run at the counted size
             }
             g_stats.pairs += npairs;
@@ -650,29 +1111,12 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
         }
         if (h_pass_new && passes < pass_cap) h_pass_new[passes] = nnew;
         if (h_rec_lits && h_rec_clause_off && h_rec_pass_off && passes + 1 < rec_pass_cap) {
-            // the pass's new clause set, each clause as ascending literals, the
-            // clauses in ascending order (deterministic whatever the append order)
             hkeys.resize((size_t)nnew * K);
             SATMI_HIP(hipMemcpyAsync(hkeys.data(), clauses.as<uint64_t>() + ncl * K, 8 * (size_t)nnew * K,
                                      hipMemcpyDeviceToHost, s));
             SATMI_HIP(hipStreamSynchronize(s));
-            std::vector<std::vector<int32_t>> pass(nnew);
-            for (int64_t c = 0; c < nnew; ++c) {
-                const uint64_t *k = hkeys.data() + c * K;
-                for (int d = 0; d < V; ++d) {
-                    if ((k[d >> 6] >> (d & 63)) & 1ull) pass[c].push_back(dense2var[d]);
-                    if ((k[W + (d >> 6)] >> (d & 63)) & 1ull) pass[c].push_back(-dense2var[d]);
-                }
-                std::sort(pass[c].begin(), pass[c].end());
-            }
-            std::sort(pass.begin(), pass.end());
-            for (const auto &cl : pass) {
-                if (rec_clauses + 1 >= rec_clause_cap || rec_lits + (int64_t)cl.size() > rec_lit_cap) break;
-                std::copy(cl.begin(), cl.end(), h_rec_lits + rec_lits);
-                rec_lits += (int64_t)cl.size();
-                h_rec_clause_off[++rec_clauses] = rec_lits;
-            }
-            h_rec_pass_off[passes + 1] = rec_clauses;
+            record_pass(hkeys, nnew, false, W, V, dense2var, passes, h_rec_lits, rec_lit_cap, h_rec_clause_off,
+                        rec_clause_cap, h_rec_pass_off, rec_clauses, rec_lits);
         }
         ++passes;
         jlo = ncl;
@@ -683,5 +1127,22 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
     *h_passes = passes;
     g_stats.pair_ms = t_pairs.total();
     g_stats.claim_ms = t_claims.total();
+    lease.ok = true;
+    return SATMI_OK;
+}
+
+// Free every idle workspace of this solver (device buffers, streams, pinned
+// words); calls in flight keep theirs.  The next call allocates afresh.
+extern "C" int satmi_resolution_trim(void) {
+    std::vector<ResWork *> idle;
+    {
+        auto &P = res_pool();
+        std::lock_guard<std::mutex> g(P.mu);
+        idle.swap(P.free_list);
+    }
+    for (ResWork *w : idle) {
+        (void)hipStreamSynchronize(w->stream);
+        delete w;
+    }
     return SATMI_OK;
 }

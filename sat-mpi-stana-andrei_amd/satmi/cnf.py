@@ -40,13 +40,19 @@ class CnfBatch:
 
 
 def pack(formulas):
-    """List of formulas (List[List[int]]) -> CnfBatch."""
+    """Formulas (an iterable of iterables of clauses of int literals) -> CnfBatch.
+    Literals must be nonzero and within int32 (INT32_MIN excluded: its negation
+    does not exist); one-shot iterables are materialised once."""
     from itertools import chain
+    formulas = [f if isinstance(f, (list, tuple)) else list(f) for f in formulas]
+    formulas = [[c if isinstance(c, (list, tuple)) else list(c) for c in f] for f in formulas]
     ncl = np.fromiter((len(f) for f in formulas), dtype=np.int64, count=len(formulas))
     clen = np.fromiter((len(c) for f in formulas for c in f), dtype=np.int64, count=int(ncl.sum()))
     lits = np.fromiter(chain.from_iterable(chain.from_iterable(formulas)), dtype=np.int64, count=int(clen.sum()))
     if lits.size and not lits.all():
         raise ValueError("literal 0 is not allowed (REF.py:51)")
+    if lits.size and (lits.max() > 2 ** 31 - 1 or lits.min() < -(2 ** 31 - 1)):
+        raise ValueError("literals must lie within +-(2^31 - 1) (int32, the library's literal type)")
     icb = np.concatenate([[0], np.cumsum(ncl)])
     clb = np.concatenate([[0], np.cumsum(clen)])
     # largest variable per formula: the max |literal| over its literal range

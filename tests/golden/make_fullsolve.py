@@ -6,6 +6,9 @@ first model:
                exhausting both branches of every decision (~40 k nodes)
     unsat200   random 3-SAT n=200, m=852: UNSAT searches of 10^5-10^6 nodes
                (~1 min on 6 cores)
+    uuf250     uuf250-shaped random 3-SAT (n=250, m=1065), node cap 5e7: the
+               UNSAT searches at n=250 that exhaust both branches of every
+               decision to the end (~1 h on 5 cores)
     python tests/golden/make_fullsolve.py [set]      (default: uf250)
 
 The checker is the C oracle (oracle/sat_oracle.c, SOUND mode), itself pinned to
@@ -33,7 +36,8 @@ from oracle import oracle  # noqa: E402
 # set: (n, m, k, seed, count, node cap) -- the fixture keeps the searches that finish within the cap
 SETS = {"uf250": (250, 1065, 3, 250, 96, 1_200_000),
         "unsat150": (150, 639, 3, 150, 24, 2_000_000),
-        "unsat200": (200, 852, 3, 200, 12, 2_000_000)}
+        "unsat200": (200, 852, 3, 200, 12, 2_000_000),
+        "uuf250": (250, 1065, 3, 2501, 16, 50_000_000)}
 SET = sys.argv[1] if len(sys.argv) > 1 else "uf250"
 N, M, K, SEED, COUNT, NODE_CAP = SETS[SET]
 OUT = os.path.join(HERE, f"fullsolve_{SET}.json")
@@ -49,7 +53,7 @@ def main():
     b = cnf.uniform_ksat(COUNT, N, M, K, seed=SEED)
     sha = hashlib.sha256(b.lits.tobytes()).hexdigest()
     cases = []
-    with ProcessPoolExecutor(max_workers=min(6, os.cpu_count() or 1)) as ex:
+    with ProcessPoolExecutor(max_workers=int(os.environ.get("FULLSOLVE_WORKERS", min(6, os.cpu_count() or 1)))) as ex:
         for i, o in ex.map(solve, range(COUNT)):
             print(i, o["status"], o["counters"]["nodes"], flush=True)
             if o["counters"]["nodes"] > NODE_CAP:

@@ -39,3 +39,16 @@ def test_menu_batch_shape():
         assert all(len({abs(l) for l in c}) == len(c) and all(1 <= abs(l) <= 15 for l in c) for c in f)
     assert 0.4 < (b.lits < 0).mean() < 0.6
     assert (cnf.menu_batch(300, 80, 3, 15, seed=7).lits == b.lits).all()
+
+
+def test_pack_rejects_out_of_range_and_accepts_iterables():
+    """Literals beyond int32 are rejected, not wrapped; generators
+    of formulas and of clauses pack like the lists they yield."""
+    import pytest
+    for bad in (2 ** 31, -(2 ** 31), 2 ** 40):
+        with pytest.raises(ValueError):
+            cnf.pack([[[1, bad]]])
+    fs = [[[1, -2], [3]], [[-4, 5, 6]]]
+    g = cnf.pack((iter(c) for c in f) for f in fs)
+    b = cnf.pack(fs)
+    assert [g.instance(i) for i in range(2)] == [b.instance(i) for i in range(2)] == fs

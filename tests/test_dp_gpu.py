@@ -10,6 +10,7 @@ import random
 import pytest
 
 import oracle
+from conftest import clause_list_sha
 from satmi import cnf
 from satmi.dp import eliminate
 
@@ -89,6 +90,29 @@ def test_php65_every_step_matches_oracle():
     assert r["clauses"] == o["clauses"][:_completed(o)]
 
 
+def test_php65_matches_reference_fixture(golden_dir):
+    """The same workload against the reference itself: the reference's own
+    davis_putnam_solver on PHP(6,5) (tests/golden/dp_php65.json,
+    make_golden_bench.py) -- the eliminated variables, the verdict, and every
+    intermediate clause list (clause order and each clause's set iteration
+    order) by length and sha256, the first four in full."""
+    with open(os.path.join(golden_dir, "dp_php65.json")) as fh:
+        (c,) = json.load(fh)["cases"]
+    r = eliminate(c["formula"], record=True)
+    assert r["result"] == int(c["result"]) == 0
+    assert r["vars"] == [s["var"] for s in c["steps"]]
+    done = [s for s in c["steps"] if "sha256" in s]
+    assert len(r["clauses"]) == len(done) == 29
+    for k, s in enumerate(done):
+        assert len(r["clauses"][k]) == s["n"], k
+        assert clause_list_sha(r["clauses"][k]) == s["sha256"], k
+        if "clauses" in s:
+            assert r["clauses"][k] == s["clauses"], k
+    # the same solve without recording (the bench path: one wait per batch)
+    r2 = eliminate(c["formula"])
+    assert (r2["result"], r2["vars"]) == (r["result"], r["vars"])
+
+
 def test_concurrent_solves_from_threads():
     """satmi_dp_host from several host threads at once (each on its own stream
     and buffers, as bench.py --threads runs it): every solve equals the oracle."""
@@ -102,3 +126,9 @@ def test_concurrent_solves_from_threads():
             for f, o, r in zip(fs, want, got):
                 assert (r["result"], r["vars"]) == (o["result"], o["vars"]), f
                 assert r["clauses"] == o["clauses"][:_completed(o)], f
+    # the pooled workspaces freed, the next solves allocate afresh
+    from satmi import _capi
+    _capi.trim_workspaces()
+    for f, o in zip(fs[:2], want[:2]):
+        r = eliminate(f, record=True)
+        assert (r["result"], r["vars"]) == (o["result"], o["vars"]) and r["clauses"] == o["clauses"][:_completed(o)]

@@ -164,16 +164,18 @@ def test_configs4_batch_properties(n, m, k, cap, B):
         assert r.counter_dict(b) == {**r.counter_dict(b), **{k_: o["counters"][k_] for k_ in CTR}}
 
 
-@pytest.mark.parametrize("fixture,min_unsat", [("uf250", 0), ("unsat150", 5), ("unsat200", 5)])
+@pytest.mark.parametrize("fixture,min_unsat", [("uf250", 0), ("unsat150", 5), ("unsat200", 5), ("uuf250", 5)])
 @pytest.mark.parametrize("split", [_capi.SPLIT_OFF, _capi.SPLIT_ALWAYS])
 def test_configs4_solved_to_completion(golden_dir, fixture, min_unsat, split):
     """configs[4]-scale searches run to the end (no node cap): uf250-shaped SAT
-    searches of 10^3-10^6 calls, and UNSAT searches at n=150 / n=200 that
-    exhaust both branches of every decision (REF.py:167-214; 10^4-10^6 calls):
-    status, every counter and the model equal the oracle's
+    searches of 10^3-10^6 calls, UNSAT searches at n=150 / n=200, and the
+    uuf250 shape itself (n=250, m=1065: 6 UNSAT searches of 2.5-8.5 M calls
+    that exhaust both branches of every decision, REF.py:167-214, beside 10
+    SAT ones): status, every counter and the model equal the oracle's
     (tests/golden/fullsolve_<fixture>.json, make_fullsolve.py), with and
     without branch splitting (a few searches on thousands of idle waves:
-    helpers take subtrees of searches a million calls deep)."""
+    helpers take subtrees of searches millions of calls deep).  Unsplit, a
+    search runs on one wavefront, so only the searches of <= 2 M calls run."""
     with open(os.path.join(golden_dir, f"fullsolve_{fixture}.json")) as fh:
         g = json.load(fh)
     batch = cnf.uniform_ksat(g["count"], g["n"], g["m"], g["k"], seed=g["seed"])
@@ -182,6 +184,9 @@ def test_configs4_solved_to_completion(golden_dir, fixture, min_unsat, split):
     cases = g["cases"]
     assert len(cases) >= 8
     assert sum(c["status"] == _capi.DPLL_EXHAUSTED for c in cases) >= min_unsat
+    if split == _capi.SPLIT_OFF:
+        cases = [c for c in cases if c["counters"]["nodes"] <= 2_000_000]
+        assert cases
     fs = [batch.instance(c["index"]) for c in cases]   # only the searches the oracle finished
     _capi.set_split(split)
     try:
@@ -473,6 +478,26 @@ def test_branch_splitting_repeated_launches_one_stream():
         rs = _run_split(batch, True, max_solutions=1, sol_cap=1)
         assert (rs.counters[:, :7] == ru.counters[:, :7]).all()
         assert (rs.sol_lits == ru.sol_lits).all()
+
+
+def test_split_stats_reset_by_a_launch_that_does_not_split():
+    """satmi_dpll_split_stats reports the stream's LAST launch: after a split
+    launch, a launch of the general kernel (REF mode) on the same stream
+    leaves the statistics all zero (include/satmi.h contract)."""
+    batch = cnf.uniform_ksat(32, 100, 426, 3, seed=99)
+    _run_split(batch, True, max_solutions=1, sol_cap=1)
+    st = _capi.split_stats(None)
+    assert st["done"] > 0 and st["donations"] > 0
+    dpll_batch([[[1, 2], [-1, 2], [1, -2]]], mode="ref", max_solutions=0, sol_cap=8)   # dpll_batch_kernel
+    assert all(v == 0 for v in _capi.split_stats(None).values())
+    _run_split(batch, True, max_solutions=1, sol_cap=1)
+    assert _capi.split_stats(None)["done"] > 0
+    _capi.set_kernel(_capi.KERNEL_WIDE)
+    try:
+        dpll_batch([[[1, 2], [-1, 2], [1, -2]]], mode="ref", max_solutions=0, sol_cap=8)   # dpll_wide_kernel
+    finally:
+        _capi.set_kernel(_capi.KERNEL_AUTO)
+    assert all(v == 0 for v in _capi.split_stats(None).values())
 
 
 @pytest.mark.parametrize("seed,nmax,kmax,mmax", [(11, 12, 4, 60), (12, 400, 300, 30)])
