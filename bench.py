@@ -220,12 +220,13 @@ def load_profile(name, key):
         return None
 
 
-def kernel_src_sha():
-    with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", "dpll_scan.hip"), "rb") as fh:
+def kernel_src_sha(kernel="dpll"):
+    src = {"dpll": "dpll_scan.hip", "cdcl": "cdcl.hip"}[kernel]
+    with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", src), "rb") as fh:
         return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
-def issue_roofline(preset, per_gpu, kernel_ms):
+def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll"):
     """The DPLL kernel's binding resource is inside the CU: issue-pipe fractions
     from the SQ counter passes kept in profiles/sq_issue.json (tools/sq_roofline.py:
     wave-instructions / LDS-array cycles per launch of this exact workload) over
@@ -245,8 +246,8 @@ def issue_roofline(preset, per_gpu, kernel_ms):
     return {"bound": bound, "achieved": a / (kernel_ms * 1e-3), "peak": p / (kernel_ms * 1e-3),
             "unit": unit + "/s", "frac": fr[bound], "fracs": fr,
             "lds_bank_conflict_share": e["lds_bank_conflict_cycles"] / e["lds_array_cycles"],
-            "clock_hz": e["effective_clock_hz"], "source": e["source"],
-            "stale": e["kernel_src_sha256_16"] != kernel_src_sha()}
+            "clock_hz": e["effective_clock_hz"], "source": e["source"], "kernel": e.get("kernel"),
+            "stale": e["kernel_src_sha256_16"] != kernel_src_sha(kernel)}
 
 
 def dpll_kernel_name(n, m, k, split):
@@ -657,10 +658,17 @@ def run_cdcl(args, world, rank, local):
     hb = hbs[0]
     pool_ex = ThreadPoolExecutor(T) if T > 1 else None
 
+    from satmi.cdcl import last_stats as cdcl_stats
+
+    def one(b):   # launch statistics are per host thread: read them in the thread that solved
+        r = cdcl_batch_packed(b, max_iter=max_iter, arrays=True)
+        r["launch"] = cdcl_stats()
+        return r
+
     def step():
         if pool_ex is None:
-            return [cdcl_batch_packed(hb, max_iter=max_iter, arrays=True)]
-        return list(pool_ex.map(lambda b: cdcl_batch_packed(b, max_iter=max_iter, arrays=True), hbs))
+            return [one(hb)]
+        return list(pool_ex.map(one, hbs))
 
     for _ in range(0 if args.profile_steps else args.warmup):
         step()
@@ -676,6 +684,9 @@ def run_cdcl(args, world, rank, local):
     elapsed = time.perf_counter() - t0
     if pool_ex is not None:
         pool_ex.shutdown()
+    launch = [r["launch"] for r in res]
+    span_ms = sum(x["span_s"] for x in launch) / len(launch) * 1e3
+    util = sum(x["busy_wave_s"] for x in launch) / sum(x["resident_waves"] * x["span_s"] for x in launch)
     el = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -696,7 +707,8 @@ def run_cdcl(args, world, rank, local):
            "sat": int((st == CDCL_SAT).sum()), "unsat": int((st == CDCL_UNSAT).sum()),
            "iteration_capped": int((st == CDCL_LIMIT).sum()),
            "iterations_per_s": iters * args.steps * world / elapsed,
-           "roofline": None}
+           "kernel_ms": span_ms, "wave_utilisation": util,
+           "roofline": issue_roofline(args.workload, nf, span_ms, kernel="cdcl")}
     r0 = res[0]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:
@@ -738,7 +750,7 @@ def legs_main(args):
         keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_issue",
                 "cpu_baseline", "result", "passes_or_steps", "instances_per_s", "unit_props_per_s",
                 "capped_fraction", "sat_fraction", "sat", "unsat", "iteration_capped", "iterations_per_s",
-                "verdict_sha")
+                "verdict_sha", "kernel_ms", "wave_utilisation")
         out[name] = {k: r[k] for k in keep if k in r}
         out[name]["leg_wall_s"] = time.perf_counter() - t
     print(json.dumps(out), flush=True)

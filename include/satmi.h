@@ -210,6 +210,12 @@ int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_clause_begin,
                           int32_t *h_status, int32_t *h_assign_len, int32_t *h_assign, int assign_stride,
                           int64_t *h_stats, double *h_var_inc);
 
+/* The calling thread's last satmi_cdcl_batch_host launch: its span on the
+ * device wall clock (first wave start to last wave end), the busy wave-time
+ * (sum over waves of the time spent solving formulas) and the resident waves;
+ * busy / (resident x span) is the launch's wave utilisation. */
+int satmi_cdcl_last_stats(double *span_s, double *busy_wave_s, int *resident_waves);
+
 /* Device-side span of the last DPLL launch on `stream`: enqueues (on that
  * stream, after the launch) a copy of two uint64 s_memrealtime ticks into
  * d_span: [0] = ~(first wave's start), [1] = last wave's end, so the launch

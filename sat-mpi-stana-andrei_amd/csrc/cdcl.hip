@@ -694,14 +694,18 @@ __global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
 #endif
     S.scratch = A.lay.lds_bytes ? (int32_t *)(cdcl_lds + A.lay.lds_scratch) : (int32_t *)(base + A.lay.scratch);
     span_begin(A.work_counter);
+    uint64_t busy = 0;   // this wave's ticks spent solving (the rest of its residency is the launch's tail)
     for (;;) {
         uint32_t b = 0;
         if (lane_id() == 0) b = atomicAdd(A.work_counter, 1u);
         b = uniform_u32(b);
         if (b >= (uint32_t)A.num_instances) break;
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
         solve_one(A, S, (int)b);
+        busy += __builtin_amdgcn_s_memrealtime() - t;
         wave_sync();
     }
+    if (lane_id() == 0) atomicAdd((unsigned long long *)A.work_counter + 3, (unsigned long long)busy);
     span_end(A.work_counter);
 }
 
@@ -794,6 +798,13 @@ CdclSlot *cdcl_acquire(int dev) {
     P.slots.push_back(c);
     return c;
 }
+// The calling thread's last satmi_cdcl_batch_host launch (satmi_cdcl_last_stats).
+struct CdclStats {
+    double span_s = 0.0, busy_wave_s = 0.0;
+    int resident_waves = 0;
+};
+thread_local CdclStats g_cdcl_stats;
+
 struct CdclSlotGuard {
     CdclSlot *c;
     ~CdclSlotGuard() {
@@ -903,7 +914,7 @@ extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_cl
             h2d(o_clb, h_clause_lit_begin, 4 * (size_t)(C + 1)) != hipSuccess ||
             h2d(o_lits, h_lits, 4 * (size_t)Ltot) != hipSuccess ||
             h2d(o_nv, nv.data(), 4 * (size_t)num_instances) != hipSuccess ||
-            hipMemsetAsync(d + o_wc, 0, 24, s) != hipSuccess) {
+            hipMemsetAsync(d + o_wc, 0, 32, s) != hipSuccess) {   // counter, span (common.h), busy ticks
             rc = hip_fail(hipGetLastError(), "satmi_cdcl_batch_host: staging");
             break;
         }
@@ -934,8 +945,20 @@ extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_cl
         d2h(h_assign, o_as, 4 * (size_t)num_instances * assign_stride);
         d2h(h_stats, o_stats, 8 * (size_t)num_instances * SATMI_CDCL_NSTATS);
         d2h(h_var_inc, o_vi, 8 * (size_t)num_instances);
+        uint64_t wc[4] = {0, 0, 0, 0};
+        d2h(wc, o_wc, sizeof(wc));
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "satmi_cdcl_batch_host: launch / copy back");
+        g_cdcl_stats.span_s = (double)(wc[2] - ~wc[1]) / ticks_per_s;
+        g_cdcl_stats.busy_wave_s = (double)wc[3] / ticks_per_s;
+        g_cdcl_stats.resident_waves = grid;
     } while (0);
     return rc;
+}
+
+extern "C" int satmi_cdcl_last_stats(double *span_s, double *busy_wave_s, int *resident_waves) {
+    if (span_s) *span_s = g_cdcl_stats.span_s;
+    if (busy_wave_s) *busy_wave_s = g_cdcl_stats.busy_wave_s;
+    if (resident_waves) *resident_waves = g_cdcl_stats.resident_waves;
+    return SATMI_OK;
 }

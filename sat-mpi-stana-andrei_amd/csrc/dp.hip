@@ -49,6 +49,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -70,6 +71,7 @@ __host__ __device__ static inline int64_t cap_for(int64_t u) {
 enum : int32_t { OVF_PAIRS = 1, OVF_NCL = 2, OVF_ARENA = 4, OVF_XS = 8 };
 
 constexpr uint64_t DP_EMPTY = ~0ull;
+constexpr int DP_STRIPES = 64;
 
 // The solve's state, on the device.  Host writes it once per solve (and on a
 // resume); kernels read sizes from it and one thread of the single-workgroup
@@ -114,6 +116,13 @@ struct DpArgs {
     int32_t *dropped, *hit;         // epoch stamps: representative subsumed by rem / survivor hit
     uint32_t *surv, *klist;         // survivors' pair indices; kept pairs in pair order
     uint64_t *rkeys, *ukeys, *skeys;  // contiguous keys: rem clauses, representatives, survivors
+    // Per-step counters striped over DP_STRIPES words each (stripe = block
+    // index mod DP_STRIPES): [0, S) representatives claimed per stripe, [S, 2S)
+    // non-tautological pairs, [2S, 3S) subset tests.  One hot counter
+    // serialises its atomics (~60 ns each under contention).  A stripe's claimed
+    // table slots go to its own region of ustage (pair_cap entries each).
+    unsigned long long *stripes;
+    uint32_t *ustage;
     uint32_t *keptbits;             // kept pairs (32 per word), cleared as compacted
     int32_t *xs;                    // per kept resolvent: AX and BY image scratch
     int64_t xs_cap;
@@ -319,32 +328,59 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
     const int W = A.W, K = A.K, dw = d >> 6, db = d & 63;
     const ClauseList L = A.g[sh_cur];
     const int64_t ncl = sh_ncl;
-    int64_t np = 0, nn = 0, nr = 0;
+    // each thread a contiguous run of clauses: its flag loads are independent
+    // (one memory latency), one block scan places every run
     int mxA = 0, mxB = 0;
-    for (int64_t b0 = 0; b0 < ncl; b0 += POP_THREADS) {
-        const int64_t c = b0 + tid;
-        const bool valid = c < ncl;
-        bool p = false, q = false;
-        if (valid) {
-            p = (L.bits[c * K + dw] >> db) & 1ull;
-            q = (L.bits[c * K + W + dw] >> db) & 1ull;
+    const int64_t per = (ncl + POP_THREADS - 1) / POP_THREADS;
+    const int64_t c0 = min<int64_t>(ncl, tid * per), c1 = min<int64_t>(ncl, c0 + per);
+    int cp = 0, cq = 0, cr = 0;
+    uint32_t fl = 0;   // bit 2k: clause c0+k holds var, bit 2k+1: -var (runs of <= 16 clauses)
+    const bool small = per <= 16;
+    for (int64_t c = c0; c < c1; ++c) {
+        const bool p = (L.bits[c * K + dw] >> db) & 1ull;
+        const bool q = (L.bits[c * K + W + dw] >> db) & 1ull;
+        if (small) fl |= (p ? 1u : 0u) << (2 * (c - c0)) | (q ? 2u : 0u) << (2 * (c - c0));
+        cp += p;
+        cq += q;
+        cr += !p && !q;
+        if (p | q) {
             const int u = L.used[c];
             if (p) mxA = max(mxA, u);
             if (q) mxB = max(mxB, u);
         }
-        int tot, tr;
-        const int ex = block_excl_scan((p ? 1 : 0) | (q ? 1 << 16 : 0), wsum, tot);
-        const int er = block_excl_scan(valid && !p && !q ? 1 : 0, wsum, tr);   // a clause may be in both lists
-        const int ep = ex & 0xFFFF, en = ex >> 16;
-        if (p) A.plist[np + ep] = c;
-        if (q) A.nlist[nn + en] = c;
-        if (valid && !p && !q) {
-            A.rlist[nr + er] = c;
-            for (int w = 0; w < K; ++w) A.rkeys[(nr + er) * K + w] = L.bits[c * K + w];
+    }
+    int tot, tr, ep, en;
+    int64_t np, nn;
+    if (ncl < 65536) {   // both counts in one scan (halves < 2^16)
+        const int ex = block_excl_scan(cp | (cq << 16), wsum, tot);
+        ep = ex & 0xFFFF;
+        en = ex >> 16;
+        np = tot & 0xFFFF;
+        nn = tot >> 16;
+    } else {
+        int tn;
+        ep = block_excl_scan(cp, wsum, tot);
+        en = block_excl_scan(cq, wsum, tn);
+        np = tot;
+        nn = tn;
+    }
+    int er = block_excl_scan(cr, wsum, tr);
+    const int64_t nr = tr;
+    for (int64_t c = c0; c < c1; ++c) {   // a clause may be in both the pos and the neg list
+        bool p, q;
+        if (small) {
+            p = (fl >> (2 * (c - c0))) & 1u;
+            q = (fl >> (2 * (c - c0) + 1)) & 1u;
+        } else {
+            p = (L.bits[c * K + dw] >> db) & 1ull;
+            q = (L.bits[c * K + W + dw] >> db) & 1ull;
         }
-        np += tot & 0xFFFF;
-        nn += tot >> 16;
-        nr += tr;
+        if (p) A.plist[ep++] = c;
+        if (q) A.nlist[en++] = c;
+        if (!p && !q) {
+            for (int w = 0; w < K; ++w) A.rkeys[er * K + w] = L.bits[c * K + w];
+            A.rlist[er++] = c;
+        }
     }
     mxA = block_max(mxA, wsum);
     mxB = block_max(mxB, wsum);
@@ -379,6 +415,7 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
         S->epoch += 1;
     }
     for (int e = tid; e < V; e += POP_THREADS) A.firstpos[e] = ~0ull;   // for the next step's assembly
+    if (tid < 3 * DP_STRIPES) A.stripes[tid] = 0ull;
 }
 
 // pair p = i*nn + j: resolvent key, tautology (REF.py:115) and empty (REF.py:117)
@@ -419,7 +456,7 @@ __global__ void __launch_bounds__(256) dp_pairs_kernel(DpArgs A) {
         cnt += lane == 0 ? __popcll(m) : 0;
     }
     const int tot = block_sum(cnt, wsum);
-    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long *)&S->nontaut, (unsigned long long)tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(A.stripes + DP_STRIPES + blockIdx.x % DP_STRIPES, (unsigned long long)tot);
 }
 
 __device__ __forceinline__ uint64_t dp_mix64(uint64_t z) {
@@ -468,11 +505,12 @@ __global__ void __launch_bounds__(256) dp_hash_kernel(DpArgs A) {
             }
         }
         const uint64_t bal = __ballot(claimed);
-        if (bal) {
+        if (bal) {   // the slot into this block's stripe region (dp_gather_kernel packs the regions)
+            const int st = blockIdx.x % DP_STRIPES;
             uint32_t base = 0;
-            if (lane == 0) base = (uint32_t)atomicAdd((unsigned long long *)&S->nuniq, (unsigned long long)__popcll(bal));
+            if (lane == 0) base = (uint32_t)atomicAdd(A.stripes + st, (unsigned long long)__popcll(bal));
             base = uniform_u32(base);
-            if (claimed) A.uslot[base + __popcll(bal & lanemask_lt())] = (uint32_t)slot;
+            if (claimed) A.ustage[(uint64_t)st * A.pair_cap + base + __popcll(bal & lanemask_lt())] = (uint32_t)slot;
         }
     }
 }
@@ -569,19 +607,33 @@ __global__ void __launch_bounds__(TEST_TILE) dp_remtest_kernel(DpArgs A) {
     int tests = 0;
     dp_test_items<KT, false>(A, S->nuniq, S->nr, A.ukeys, A.rkeys, nullptr, A.dropped, S->epoch, tests);
     const int tot = block_sum(tests, wsum);
-    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long *)&S->tests, (unsigned long long)tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(A.stripes + 2 * DP_STRIPES + blockIdx.x % DP_STRIPES, (unsigned long long)tot);
 }
 
-// the keys of the distinct representatives, contiguous (remtest's x side)
+// the distinct representatives, packed from the stripe regions: their table
+// slots (uslot) and keys (ukeys, remtest's x side), contiguous; nuniq.  Grid:
+// x blocks per stripe, DP_STRIPES in y.
 __global__ void __launch_bounds__(256) dp_gather_kernel(DpArgs A) {
+    __shared__ int64_t pre[DP_STRIPES + 1];
     DpState *S = A.st;
     if (S->done || S->first_empty != DP_EMPTY) return;
-    const int64_t nuniq = S->nuniq;
-    const int K = A.K;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nuniq * K; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t u = e / K;
-        const uint64_t p = A.table[A.uslot[u]];
-        A.ukeys[e] = A.rbits[p * K + (e - u * K)];
+    if (threadIdx.x == 0) {
+        int64_t acc = 0;
+        for (int t = 0; t < DP_STRIPES; ++t) {
+            pre[t] = acc;
+            acc += (int64_t)A.stripes[t];
+        }
+        pre[DP_STRIPES] = acc;
+        if (blockIdx.x == 0 && blockIdx.y == 0) S->nuniq = acc;
+    }
+    __syncthreads();
+    const int st = blockIdx.y, K = A.K;
+    const int64_t n = pre[st + 1] - pre[st], u0 = pre[st];
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t slot = A.ustage[(uint64_t)st * A.pair_cap + t];
+        A.uslot[u0 + t] = slot;
+        const uint64_t p = A.table[slot];
+        for (int w = 0; w < K; ++w) A.ukeys[(u0 + t) * K + w] = A.rbits[p * K + w];
     }
 }
 
@@ -592,9 +644,13 @@ __global__ void __launch_bounds__(256) dp_survlist_kernel(DpArgs A) {
     if (S->done || S->first_empty != DP_EMPTY) return;
     const int64_t nuniq = S->nuniq;
     const int32_t epoch = S->epoch;
-    const int lane = lane_id(), K = A.K;
-    for (int64_t u0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); u0 < nuniq; u0 += (int64_t)gridDim.x * 256) {
-        const int64_t u = u0 + lane;
+    const int lane = lane_id(), K = A.K, tid = threadIdx.x;
+    __shared__ int wcnt[4];
+    __shared__ uint32_t bbase;
+    // one block round: 256 representatives; the block's survivors take ONE
+    // append atomic (a hot counter serialises)
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < nuniq; b0 += (int64_t)gridDim.x * 256) {   // block-uniform
+        const int64_t u = b0 + tid;
         bool keep = false;
         uint32_t p = 0;
         if (u < nuniq) {
@@ -604,16 +660,18 @@ __global__ void __launch_bounds__(256) dp_survlist_kernel(DpArgs A) {
             keep = A.dropped[u] != epoch;
         }
         const uint64_t bal = __ballot(keep);
-        if (bal) {
-            uint32_t base = 0;
-            if (lane == 0) base = (uint32_t)atomicAdd((unsigned long long *)&S->nsurv, (unsigned long long)__popcll(bal));
-            base = uniform_u32(base);
-            if (keep) {
-                const uint32_t at = base + __popcll(bal & lanemask_lt());
-                A.surv[at] = p;
-                for (int w = 0; w < K; ++w) A.skeys[(uint64_t)at * K + w] = A.ukeys[u * K + w];
-            }
+        if (lane == 0) wcnt[tid >> 6] = __popcll(bal);
+        __syncthreads();
+        const int nb = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        if (tid == 0 && nb) bbase = (uint32_t)atomicAdd((unsigned long long *)&S->nsurv, (unsigned long long)nb);
+        __syncthreads();
+        if (keep) {
+            uint32_t at = bbase + __popcll(bal & lanemask_lt());
+            for (int w = 0; w < (tid >> 6); ++w) at += wcnt[w];
+            A.surv[at] = p;
+            for (int w = 0; w < K; ++w) A.skeys[(uint64_t)at * K + w] = A.ukeys[u * K + w];
         }
+        __syncthreads();
     }
 }
 
@@ -627,7 +685,7 @@ __global__ void __launch_bounds__(TEST_TILE) dp_survtest_kernel(DpArgs A) {
     int tests = 0;
     dp_test_items<KT, true>(A, S->nsurv, S->nsurv, A.skeys, A.skeys, A.surv, A.hit, S->epoch, tests);
     const int tot = block_sum(tests, wsum);
-    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long *)&S->tests, (unsigned long long)tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(A.stripes + 2 * DP_STRIPES + blockIdx.x % DP_STRIPES, (unsigned long long)tot);
 }
 
 // One workgroup: the step's verdict (the first empty resolvent, or the clause
@@ -640,7 +698,21 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
     if (S->done) return;
     const int tid = threadIdx.x;
     const uint64_t fe = S->first_empty;
-    const int64_t npairs = S->npairs, nr = S->nr, nontaut = S->nontaut;
+    __shared__ int64_t sh_nt;
+    if (tid < 64) {   // the striped counters of this step (one wave)
+        int64_t nt = (int64_t)A.stripes[DP_STRIPES + tid], ts = (int64_t)A.stripes[2 * DP_STRIPES + tid];
+        for (int o = 32; o >= 1; o >>= 1) {
+            nt += __shfl_xor(nt, o);
+            ts += __shfl_xor(ts, o);
+        }
+        if (tid == 0) {
+            sh_nt = nt;
+            S->nontaut = nt;
+            S->tests += ts;
+        }
+    }
+    __syncthreads();
+    const int64_t npairs = S->npairs, nr = S->nr, nontaut = sh_nt;
     // clause_limit: the reference stops when remaining + new passes the limit,
     // i.e. at the kth non-tautological non-empty pair (0-based)
     int64_t limit_pair = -1;
@@ -899,6 +971,19 @@ struct DpStats {
 };
 thread_local DpStats g_dp_stats;   // the calling thread's last call
 
+// The captured step batch of a workspace (see satmi_dp_host).
+struct DpGraph {
+    hipGraphExec_t exec = nullptr;
+    DpArgs args;
+    int batch = 0;
+    DpGraph() { std::memset(&args, 0, sizeof(args)); }
+    void reset() {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        exec = nullptr;
+        batch = 0;
+    }
+};
+
 // Device buffers of one solve, kept between calls (grow-only) in a process-wide
 // pool: a call takes a free workspace (or makes one) and returns it when done,
 // so concurrent calls from any number of threads each own one and the number
@@ -906,7 +991,7 @@ thread_local DpStats g_dp_stats;   // the calling thread's last call
 struct DpWork {
     Buf d_off, d_lits, d_v2d, d_d2v, state, firstpos, order, popscratch, trace;
     Buf plist, nlist, rlist, rbits, ntbits, table, uslot, dropped, hit, surv, klist, keptbits, xs, arena;
-    Buf rkeys, ukeys, skeys;
+    Buf rkeys, ukeys, skeys, ustage, stripes;
     Gen g[2];
     int64_t ncl_cap = 0, pair_cap = 0, arena_cap = 0, xs_cap = 0;
     uint64_t tslots = 0;
@@ -916,7 +1001,9 @@ struct DpWork {
     hipStream_t stream = nullptr;
     DpState *pin = nullptr;       // pinned host copy of the state
     int dev = 0;
-    ~DpWork() {   // only a workspace that failed mid-call is destroyed (after its stream drained)
+    DpGraph graph;
+    ~DpWork() {   // only a workspace that failed mid-call (or a trim) destroys one, after its stream drained
+        graph.reset();
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         if (pin) (void)hipHostFree(pin);
@@ -989,6 +1076,7 @@ int grow_pairs(DpWork &W, int64_t npairs, int K) {
     DP_TRY(W.surv.need(4 * (size_t)cap, s));
     DP_TRY(W.klist.need(4 * (size_t)cap, s));
     DP_TRY(W.ukeys.need(8 * (size_t)cap * K, s));
+    DP_TRY(W.ustage.need(4 * (size_t)DP_STRIPES * cap, s));
     DP_TRY(W.skeys.need(8 * (size_t)cap * K, s));
     DP_TRY(W.dropped.need(4 * (size_t)cap, s, 0, 0));
     DP_TRY(W.hit.need(4 * (size_t)cap, s, 0, 0));
@@ -1005,6 +1093,7 @@ int grow_pairs(DpWork &W, int64_t npairs, int K) {
     W.pair_cap = std::min<int64_t>((int64_t)(W.rbits.cap / (8 * (size_t)K)), (int64_t)(W.tslots / 2));
     W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.uslot.cap / 4));
     W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.ukeys.cap / (8 * (size_t)K)));
+    W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.ustage.cap / (4 * (size_t)DP_STRIPES)));
     W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.skeys.cap / (8 * (size_t)K)));
     W.pair_cap = std::min<int64_t>(W.pair_cap, (1ll << 31) - 1);
     W.K = K;
@@ -1105,6 +1194,7 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     const int64_t popcap = cap_for(V);
     DP_TRY(Wk.popscratch.need(4 * (size_t)2 * popcap, s));
     DP_TRY(Wk.trace.need(4 * (size_t)(V + 1), s));
+    DP_TRY(Wk.stripes.need(8 * 3 * DP_STRIPES, s, 0, 0));
     DP_TRY(grow_ncl(Wk, std::max<int64_t>(nclauses, 1), K, 0, 0));
     DP_TRY(grow_pairs(Wk, 1, K));
     const int64_t arena0 = (int64_t)nclauses * 2 * cap0;
@@ -1132,6 +1222,7 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     (void)satmi_wallclock_hz(&hz);
     const auto args = [&]() {
         DpArgs a;
+        std::memset(&a, 0, sizeof(a));   // padding too: a batch's graph is keyed by these bytes
         a.st = Wk.state.as<DpState>();
         a.g[0] = Wk.g[0].view();
         a.g[1] = Wk.g[1].view();
@@ -1163,6 +1254,8 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         a.rkeys = Wk.rkeys.as<uint64_t>();
         a.ukeys = Wk.ukeys.as<uint64_t>();
         a.skeys = Wk.skeys.as<uint64_t>();
+        a.stripes = Wk.stripes.as<unsigned long long>();
+        a.ustage = Wk.ustage.as<uint32_t>();
         a.keptbits = Wk.keptbits.as<uint32_t>();
         a.xs = Wk.xs.as<int32_t>();
         a.xs_cap = Wk.xs_cap;
@@ -1179,7 +1272,8 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
                            Wk.d_off.as<int32_t>(), Wk.d_lits.as<int32_t>(), cap0);
         SATMI_HIP(hipGetLastError());
     }
-    size_t nev = 0;   // filter timing event pairs recorded this call
+    // device time of the elimination steps: one event pair per batch
+    size_t nev = 0;
     const auto next_events = [&]() -> hipEvent_t * {
         if (2 * nev + 2 > Wk.ev.size()) {
             hipEvent_t a = nullptr, b = nullptr;
@@ -1195,14 +1289,9 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         const int gc = (int)std::min<int64_t>(2048, (a.ncl_cap + ASM_WAVES - 1) / ASM_WAVES);
         hipLaunchKernelGGL(dp_pop_split_kernel, dim3(1), dim3(POP_THREADS), 0, s, a);
         hipLaunchKernelGGL(dp_pairs_kernel, dim3(gp), dim3(256), 0, s, a);
-        hipEvent_t *ev = next_events();
-        if (!ev) {
-            set_error("satmi_dp_host: hipEventCreate failed");
-            return SATMI_ERR_HIP;
-        }
-        SATMI_HIP(hipEventRecord(ev[0], s));
         hipLaunchKernelGGL(dp_hash_kernel, dim3(gp), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(dp_gather_kernel, dim3(gp), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(dp_gather_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(64, a.pair_cap / (DP_STRIPES * 256))), DP_STRIPES),
+                           dim3(256), 0, s, a);
         const dim3 gt((unsigned)std::min<int64_t>(2048, std::max<int64_t>(64, a.pair_cap / 256)));
         switch (a.K) {
             case 2: hipLaunchKernelGGL(dp_remtest_kernel<2>, gt, dim3(TEST_TILE), 0, s, a); break;
@@ -1219,7 +1308,6 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             case 8: hipLaunchKernelGGL(dp_survtest_kernel<8>, gt, dim3(TEST_TILE), 0, s, a); break;
             default: hipLaunchKernelGGL(dp_survtest_kernel<0>, gt, dim3(TEST_TILE), 0, s, a);
         }
-        SATMI_HIP(hipEventRecord(ev[1], s));
         hipLaunchKernelGGL(dp_kept_kernel, dim3(1), dim3(POP_THREADS), 0, s, a);
         hipLaunchKernelGGL(dp_assemble_kernel, dim3(gc), dim3(64 * ASM_WAVES), 0, s, a);
         SATMI_HIP(hipGetLastError());
@@ -1234,7 +1322,41 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     for (;;) {
         // at most V steps eliminate a variable, then one pop finds the set empty
         const int batch = record ? 1 : std::min(64, V + 1);
-        for (int k = 0; k < batch; ++k) DP_TRY(enqueue_step(A));
+        hipEvent_t *ev = next_events();
+        if (!ev) {
+            set_error("satmi_dp_host: hipEventCreate failed");
+            return SATMI_ERR_HIP;
+        }
+        SATMI_HIP(hipEventRecord(ev[0], s));
+        // A batch is ~10 launches per step whose arguments depend only on the
+        // workspace and the call's limits: the second time the same batch is
+        // enqueued it is captured into a HIP graph, and from then on replayed
+        // with one launch (the steps' sizes live on the device either way).
+        DpGraph &G = Wk.graph;
+        const bool same = G.batch == batch && std::memcmp(&G.args, &A, sizeof(DpArgs)) == 0;
+        if (!record && same && G.exec) {
+            SATMI_HIP(hipGraphLaunch(G.exec, s));
+        } else if (!record && same) {
+            hipGraph_t graph = nullptr;
+            SATMI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            int rc = SATMI_OK;
+            for (int k = 0; k < batch && rc == SATMI_OK; ++k) rc = enqueue_step(A);
+            const hipError_t ec = hipStreamEndCapture(s, &graph);
+            if (rc != SATMI_OK) return rc;
+            SATMI_HIP(ec);
+            const hipError_t ei = hipGraphInstantiate(&G.exec, graph, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(graph);
+            SATMI_HIP(ei);
+            SATMI_HIP(hipGraphLaunch(G.exec, s));
+        } else {
+            if (!record) {   // remember the batch: captured if it comes again
+                G.reset();
+                G.args = A;
+                G.batch = batch;
+            }
+            for (int k = 0; k < batch; ++k) DP_TRY(enqueue_step(A));
+        }
+        SATMI_HIP(hipEventRecord(ev[1], s));
         enqueued += batch;
         SATMI_HIP(hipMemcpyAsync(Wk.pin, Wk.state.p, sizeof(DpState), hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));

@@ -301,7 +301,7 @@ __global__ void res_append_kernel(const uint64_t *cand, const int64_t *flag, con
 // on the device (ResState); the host enqueues passes without waiting.
 struct ResState {
     int64_t ncl, jlo;             // clauses; first clause added by the previous pass
-    unsigned long long count;     // claims of the running pass (starts at slot_base)
+    unsigned long long count;     // claims of the last pass
     int64_t passes;
     int64_t pairs, candidates;    // whole saturation
     uint64_t t0;                  // s_memrealtime at the start
@@ -319,9 +319,20 @@ struct ResArgs {
     int64_t max_passes, clause_limit;
     uint64_t limit_ticks;
     int64_t slot_base;   // test knob (satmi_resolution_debug_slot_base)
+    // A pass's new keys are appended to RES_STRIPES staging regions (stripe =
+    // block index mod RES_STRIPES, each with its own counter): one hot counter
+    // serialises its atomics (~60 ns each under contention), so the appends are
+    // spread over many, and res_gather_kernel packs the regions after the pass.
+    uint64_t *stage;
+    int64_t stage_region;            // keys per stripe region
+    unsigned long long *stripes;     // [RES_STRIPES] append counts (from slot_base), [RES_STRIPES] candidates
 };
+constexpr int RES_STRIPES = 64;
 
-constexpr int RES_PROBE_MAX = 1 << 12;   // buckets: a probe run this long means the table is too full
+// A probe run of this many full buckets means the table is filling up (at
+// load <= 1/2 it practically never happens): the pass stops as an overflow and
+// runs again on a larger table -- instead of probing a full table for ever.
+constexpr int RES_PROBE_MAX = 32;
 constexpr int RES_BUCKET = 8;             // slots per bucket: one 64-B read checks them all
 
 __global__ void __launch_bounds__(256) res_pack_kernel(const uint64_t *k2, int64_t n, uint64_t *keys, ResState *S) {
@@ -369,15 +380,20 @@ __global__ void __launch_bounds__(256) res_seed_kernel(uint64_t *table, uint64_t
         if (bucket_claim(table, bmask, keys[c]) < 0) S->overflow = 1;
 }
 
-// One pass (REF.py:67-95): the pairs (i < j), j in [jlo, ncl), numbered
-// g = j(j-1)/2 + i, one pair per thread (grid-stride rounds): the lanes of a
-// wave share j (one broadcast key load) and read consecutive keys i, and no
-// thread walks a serial chain of probes.  A block's new keys collect in an LDS
-// buffer and are appended with ONE atomic on the pass's counter per flush (a
-// single global counter serialises: one atomic per wavefront with a claim was
-// the kernel's bound).
-constexpr int RES_ABUF = 2048;
+// One pass (REF.py:67-95) over the pairs (i < j), j in [jlo, ncl), in tiles of
+// tj clauses j x 256 clauses i: block (x, y) takes j-tiles x, x + gx, ... and
+// i-tiles y, y + gy, ... (tiles above the diagonal exit at once).  The tile's
+// j keys sit in LDS (read by broadcast), each lane holds one key i and walks
+// the tile's j's -- a key is read from memory once per tile.  tj adapts to the
+// pass (about RES_TILES tiles, 1 <= tj <= RES_TJ): a small pass gets short
+// tiles (no lane walks a long chain of probes), a large one long tiles.  A
+// tile's new keys collect in an LDS buffer and are appended with ONE atomic
+// on the pass's counter (a single global counter serialises: one atomic per
+// wavefront with a claim was the kernel's bound).
+constexpr int RES_TJ = 32, RES_ABUF = 1024;
+constexpr int64_t RES_TILES = 16384;
 __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
+    __shared__ uint64_t jk[RES_TJ];
     __shared__ uint64_t abuf[RES_ABUF];
     __shared__ int wsum[4];
     __shared__ int sh_stop, an;
@@ -387,28 +403,15 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
     const int64_t jlo = S->jlo, ncl = S->ncl;
     const uint64_t t0 = S->t0;
     const int ln = lane_id(), tid = threadIdx.x;
-    const int64_t g0 = jlo * (jlo - 1) / 2, T = ncl * (ncl - 1) / 2 - g0;   // this pass's pairs
-    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int stripe = (int)((blockIdx.y * gridDim.x + blockIdx.x) % RES_STRIPES);
+    // tiles ~ (ncl - jlo) / tj x ncl / 512 (the triangle) ~ RES_TILES
+    const int tj = (int)max<int64_t>(1, min<int64_t>(RES_TJ, (ncl - jlo) * (ncl / 512 + 1) / RES_TILES));
     int cand = 0;
-    if (tid == 0) an = 0;
-    // flush the buffered keys (block-uniform call)
-    const auto flush = [&]() {
-        const int na = min(an, RES_ABUF);
-        if (tid == 0 && na) abase = atomicAdd(&S->count, (unsigned long long)na);
-        __syncthreads();
-        const int64_t first = (int64_t)(abase - (unsigned long long)A.slot_base);
-        for (int t = tid; t < na; t += 256) {
-            if (ncl + first + t < A.key_cap)
-                A.keys[ncl + first + t] = abuf[t];
-            else
-                __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (tid == 0) an = 0;
-    };
-    int round = 0;
-    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < T; b0 += stride, ++round) {   // block-uniform
-        if ((round & 15) == 0) {
+    const int64_t njt = (ncl - jlo + tj - 1) / tj;
+    for (int64_t jt = blockIdx.x; jt < njt; jt += gridDim.x) {
+        const int64_t j0 = jlo + jt * tj, j1 = min<int64_t>(j0 + tj, ncl);
+        const int nj = (int)(j1 - j0);
+        for (int64_t i0 = (int64_t)blockIdx.y * 256; i0 < j1 - 1; i0 += (int64_t)gridDim.y * 256) {
             if (tid == 0) {
                 int stop = __hip_atomic_load(&S->empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
                            __hip_atomic_load(&S->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -417,71 +420,116 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
                     stop = 1;
                 }
                 sh_stop = stop;
+                an = 0;
             }
+            if (tid < nj) jk[tid] = A.keys[j0 + tid];
             __syncthreads();
-            if (sh_stop) break;
-        }
-        const int64_t t = b0 + tid;
-        bool win = false;
-        uint64_t r = 0;
-        if (t < T) {
-            const int64_t g = g0 + t;
-            int64_t j = (int64_t)(0.5 + sqrt(0.25 + 2.0 * (double)g));   // j(j-1)/2 <= g < j(j+1)/2
-            while (j * (j - 1) / 2 > g) --j;
-            while (j * (j + 1) / 2 <= g) ++j;
-            const int64_t i = g - j * (j - 1) / 2;
-            const uint64_t a = A.keys[i], b = A.keys[j];
-            const uint32_t Pa = (uint32_t)a, Na = (uint32_t)(a >> 32), Pb = (uint32_t)b, Nb = (uint32_t)(b >> 32);
-            const uint32_t clash = (Pa & Nb) | (Na & Pb);
-            // exactly one clashing variable: the resolvent (two or more make
-            // every resolvent a tautology, REF.py:81)
-            if (clash && !(clash & (clash - 1))) {
-                const uint32_t P = (Pa | Pb) & ~clash, N = (Na | Nb) & ~clash;
-                if (!(P & N)) {
-                    if (!(P | N)) {
-                        __hip_atomic_store(&S->empty, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // REF.py:84-85
-                    } else {
-                        ++cand;
-                        r = (uint64_t)P | ((uint64_t)N << 32);
-                        const int c = bucket_claim(A.table, A.tmask, r);
-                        win = c > 0;
-                        if (c < 0) __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (sh_stop) break;   // block-uniform
+            const int64_t i = i0 + tid;
+            const uint64_t a = i < j1 ? A.keys[i] : 0ull;
+            const uint32_t Pa = (uint32_t)a, Na = (uint32_t)(a >> 32);
+            const int first = (int)max<int64_t>(0, i + 1 - j0);   // j's of this tile above i
+            for (int jj = 0; jj < nj; ++jj) {
+                bool win = false;
+                uint64_t r = 0;
+                if (jj >= first && i < j1) {
+                    const uint64_t b = jk[jj];
+                    const uint32_t Pb = (uint32_t)b, Nb = (uint32_t)(b >> 32);
+                    const uint32_t clash = (Pa & Nb) | (Na & Pb);
+                    // exactly one clashing variable: the resolvent (two or more
+                    // make every resolvent a tautology, REF.py:81)
+                    if (clash && !(clash & (clash - 1))) {
+                        const uint32_t P = (Pa | Pb) & ~clash, N = (Na | Nb) & ~clash;
+                        if (!(P & N)) {
+                            if (!(P | N)) {
+                                __hip_atomic_store(&S->empty, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // REF.py:84-85
+                            } else {
+                                ++cand;
+                                r = (uint64_t)P | ((uint64_t)N << 32);
+                                const int c = bucket_claim(A.table, A.tmask, r);
+                                win = c > 0;
+                                if (c < 0) __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                        }
+                    }
+                }
+                const uint64_t m = __ballot(win);
+                if (m) {   // clauses.extend(new), staged in the tile's LDS buffer
+                    int pos = 0;
+                    if (ln == 0) pos = atomicAdd(&an, __popcll(m));
+                    pos = __shfl(pos, 0) + __popcll(m & lanemask_lt());
+                    if (win) {
+                        if (pos < RES_ABUF) {
+                            abuf[pos] = r;
+                        } else {   // a full buffer (rare): append directly
+                            const int64_t idx =
+                                (int64_t)(atomicAdd(A.stripes + stripe, 1ull) - (unsigned long long)A.slot_base);
+                            if (idx < A.stage_region)
+                                A.stage[stripe * A.stage_region + idx] = r;
+                            else
+                                __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
                     }
                 }
             }
+            __syncthreads();
+            const int na = min(an, RES_ABUF);
+            if (na) {   // the tile's new keys: one append atomic on the block's stripe
+                if (tid == 0) abase = atomicAdd(A.stripes + stripe, (unsigned long long)na);
+                __syncthreads();
+                const int64_t f0 = (int64_t)(abase - (unsigned long long)A.slot_base);
+                for (int t = tid; t < na; t += 256) {
+                    if (f0 + t < A.stage_region)
+                        A.stage[stripe * A.stage_region + f0 + t] = abuf[t];
+                    else
+                        __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            __syncthreads();   // jk / abuf / sh_stop are rewritten by the next tile
         }
-        const uint64_t m = __ballot(win);
-        if (m) {   // clauses.extend(new), staged in the block's LDS buffer
-            int pos = 0;
-            if (ln == 0) pos = atomicAdd(&an, __popcll(m));
-            pos = __shfl(pos, 0) + __popcll(m & lanemask_lt());
-            if (win) abuf[pos] = r;   // room: flushed below before it can fill
-        }
-        __syncthreads();
-        if (an > RES_ABUF - 256) flush();   // block-uniform: an settled by the barrier
     }
-    __syncthreads();
-    flush();
     int tot;
     {   // block sum of the candidates (every thread reaches here)
-        const int wid = tid >> 6;
         const int incl = wave_incl_scan(cand);
-        if (ln == 63) wsum[wid] = incl;
+        if (ln == 63) wsum[tid >> 6] = incl;
         __syncthreads();
         tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     }
-    if (tid == 0 && tot) atomicAdd((unsigned long long *)&S->candidates, (unsigned long long)tot);
+    if (tid == 0 && tot) atomicAdd(A.stripes + RES_STRIPES + stripe, (unsigned long long)tot);
 }
 
-// after a pass (one thread): the verdict or the next pass's bounds
-__global__ void res_finish_pass_kernel(ResArgs A) {
+// the pass's new keys, packed from the stripe regions after the clause list
+// (grid: x blocks per stripe, RES_STRIPES in y)
+__global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
+    __shared__ int64_t pre[RES_STRIPES + 1];
     ResState *S = A.st;
-    if (S->done) return;
+    if (S->done || S->overflow) return;
+    if (threadIdx.x == 0) {
+        int64_t acc = 0;
+        for (int t = 0; t < RES_STRIPES; ++t) {
+            pre[t] = acc;
+            acc += (int64_t)(A.stripes[t] - (unsigned long long)A.slot_base);
+        }
+        pre[RES_STRIPES] = acc;
+    }
+    __syncthreads();
+    const int st = blockIdx.y;
+    const int64_t ncl = S->ncl, n = pre[st + 1] - pre[st];
+    if (ncl + pre[RES_STRIPES] > A.key_cap) {   // the next clause list does not fit the key buffer
+        if (blockIdx.x == 0 && threadIdx.x == 0 && st == 0)
+            __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+        A.keys[ncl + pre[st] + t] = A.stage[st * A.stage_region + t];
+}
+
+// the verdict of a pass with nnew new clauses, or the next pass's bounds
+__device__ void finish_pass(const ResArgs &A, ResState *S, int64_t nnew) {
     if (S->overflow) {   // the host grows the buffers and runs this pass again
         S->done = 1;
         return;
     }
-    const int64_t nnew = (int64_t)(S->count - (unsigned long long)A.slot_base);
     S->pairs += (S->ncl * (S->ncl - 1) - S->jlo * (S->jlo - 1)) / 2;
     if (S->empty) {   // an empty resolvent: unsatisfiable (REF.py:84-85)
         S->result = 0;
@@ -501,9 +549,31 @@ __global__ void res_finish_pass_kernel(ResArgs A) {
     S->passes += 1;
     S->jlo = S->ncl;
     S->ncl += nnew;
-    S->count = (unsigned long long)A.slot_base;
     if ((A.max_passes > 0 && S->passes >= A.max_passes) || (A.clause_limit > 0 && S->ncl > A.clause_limit))
         S->done = 1;   // result stays -1
+}
+
+// after a pass (one workgroup of RES_STRIPES threads): the claims summed over
+// the stripes, the verdict or the next pass's bounds; the counters reset
+__global__ void __launch_bounds__(RES_STRIPES) res_finish_pass_kernel(ResArgs A) {
+    __shared__ int64_t cnt[RES_STRIPES], cand[RES_STRIPES];
+    ResState *S = A.st;
+    const int t = threadIdx.x;
+    cnt[t] = (int64_t)(A.stripes[t] - (unsigned long long)A.slot_base);
+    cand[t] = (int64_t)A.stripes[RES_STRIPES + t];
+    A.stripes[t] = (unsigned long long)A.slot_base;
+    A.stripes[RES_STRIPES + t] = 0ull;
+    __syncthreads();
+    if (t != 0) return;
+    int64_t claims = 0, cands = 0;
+    for (int k = 0; k < RES_STRIPES; ++k) {
+        claims += cnt[k];
+        cands += cand[k];
+    }
+    if (S->done) return;
+    S->count = (unsigned long long)claims;   // this pass's claims (a regrowth is sized by them)
+    S->candidates += cands;
+    finish_pass(A, S, claims);
 }
 
 // ------------------------------------------------------------------ host side
@@ -609,7 +679,7 @@ struct EventTimer {
 // so allocating its buffers per call cost more than its kernels.
 struct ResWork {
     DevBuf d_off, d_lits, d_map, clauses, cand, counters, table, flag, pos, slotv, tiles, grand;
-    DevBuf keys, state, passnew;   // the packed path
+    DevBuf keys, state, passnew, stage, stripes;   // the packed path
     EventTimer t_pairs, t_claims;
     hipStream_t stream = nullptr;
     unsigned long long *pin = nullptr;   // pinned host words: the per-chunk counters and claim count
@@ -731,7 +801,13 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     SATMI_TRY(wk.keys.reserve(8 * (size_t)std::max<int64_t>(4 * (int64_t)nclauses, 1 << 14)));
     SATMI_TRY(wk.state.reserve(sizeof(ResState)));
     SATMI_TRY(wk.passnew.reserve(8 * (size_t)PCAP));
+    SATMI_TRY(wk.stripes.reserve(8 * 2 * RES_STRIPES));
     int64_t key_cap = (int64_t)(wk.keys.cap / 8);
+    // stripe regions: twice the key room (the stripes fill unevenly)
+    SATMI_TRY(wk.stage.reserve(8 * 2 * (size_t)key_cap));
+    std::vector<unsigned long long> stripes0(2 * RES_STRIPES, 0ull);
+    for (int t = 0; t < RES_STRIPES; ++t) stripes0[t] = (unsigned long long)slot_base;
+    SATMI_HIP(hipMemcpyAsync(wk.stripes.p, stripes0.data(), 8 * 2 * RES_STRIPES, hipMemcpyHostToDevice, s));
     // the table: a power of two >= 2x the keys it can hold (load <= 1/2; a
     // table larger than needed only spreads the probes over more cache lines)
     const auto slots_for = [](int64_t nkeys) {   // a power of two, >= 8 buckets
@@ -747,7 +823,6 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     ResState &st = *wk.pst;
     st = ResState{};
     st.ncl = nclauses;
-    st.count = (unsigned long long)slot_base;
     st.result = -1;
     // the deadline is measured on the device from the pack kernel's start (t0
     // written by it): copy the state behind it without t0
@@ -783,6 +858,9 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         A.clause_limit = clause_limit;
         A.limit_ticks = time_limit_s > 0 ? (uint64_t)std::max(1.0, time_limit_s * hz) : 0;
         A.slot_base = slot_base;
+        A.stage = wk.stage.as<uint64_t>();
+        A.stage_region = (int64_t)(wk.stage.cap / 8) / RES_STRIPES;
+        A.stripes = wk.stripes.as<unsigned long long>();
     };
     args();
     EventTimer &t_pairs = wk.t_pairs;
@@ -791,7 +869,7 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     const bool record = h_rec_lits && h_rec_clause_off && h_rec_pass_off;
     int64_t rec_clauses = 0, rec_lits = 0;
     std::vector<uint64_t> hkeys;
-    const dim3 pass_grid(4096);   // grid-stride rounds of 256 pairs per block
+    const dim3 pass_grid(256, 32);   // j-tiles x i-tiles, grid-stride
     for (;;) {
         // passes per wait: all of them when the count is bounded (<= 16)
         const int64_t left = max_passes > 0 ? max_passes - st.passes : 4;
@@ -801,18 +879,20 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
             t_pairs.begin(s);
             hipLaunchKernelGGL(res_pass_packed_kernel, pass_grid, dim3(256), 0, s, A);
             t_pairs.end(s);
-            hipLaunchKernelGGL(res_finish_pass_kernel, dim3(1), dim3(1), 0, s, A);
+            hipLaunchKernelGGL(res_gather_kernel, dim3(8, RES_STRIPES), dim3(256), 0, s, A);
+            hipLaunchKernelGGL(res_finish_pass_kernel, dim3(1), dim3(RES_STRIPES), 0, s, A);
         }
         SATMI_HIP(hipGetLastError());
         SATMI_HIP(hipMemcpyAsync(wk.pst, wk.state.p, sizeof(ResState), hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
         if (st.overflow) {   // grow the key buffer and / or the table, re-seed, run the pass again
-            // the claims of the stopped pass (all of its new keys when only
-            // the key buffer ran out) plus a quarter
-            const int64_t claims = (int64_t)(st.count - (unsigned long long)slot_base);
-            const int64_t want = std::max<int64_t>(key_cap + key_cap / 2, st.ncl + claims + claims / 4 + 1024);
+            // twice the claims of the stopped pass (all of its new keys when
+            // only the key buffer ran out; a part of them when it stopped early)
+            const int64_t claims = (int64_t)st.count;
+            const int64_t want = std::max<int64_t>(2 * key_cap, st.ncl + 2 * claims + 1024);
             SATMI_TRY(grow_keys(wk, want, st.ncl, s));
             key_cap = (int64_t)(wk.keys.cap / 8);
+            SATMI_TRY(wk.stage.reserve(8 * 2 * (size_t)key_cap));   // (the finish kernel reset the stripes)
             tslots = slots_for(key_cap);
             SATMI_TRY(wk.table.reserve(8 * tslots));
             args();
@@ -820,7 +900,7 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
             st.done = 0;
             st.empty = 0;
             st.timeout = 0;
-            st.count = (unsigned long long)slot_base;
+            st.count = 0;
             SATMI_HIP(hipMemcpyAsync(wk.state.p, wk.pst, sizeof(ResState), hipMemcpyHostToDevice, s));
             SATMI_TRY(seed(st.ncl));   // (after the state: a seed overflow flag must survive)
             continue;

@@ -31,7 +31,7 @@ EXPORTED = (
     "satmi_dpll_launch_span", "satmi_wallclock_hz", "satmi_resolution_debug_slot_base",
     "satmi_resolution_last_stats", "satmi_dpll_set_split", "satmi_dpll_split_stats", "satmi_dp_last_stats",
     "satmi_cdcl_batch_host", "satmi_dpll_set_split_warmup", "satmi_resolution_debug_cand_bytes",
-    "satmi_dp_trim", "satmi_resolution_trim",
+    "satmi_dp_trim", "satmi_resolution_trim", "satmi_cdcl_last_stats",
 )
 
 
@@ -126,6 +126,7 @@ def load():
         i32p, i32p, i64p, ctypes.c_int, i32p, ctypes.c_int64, i64p, ctypes.c_int64, i64p, ctypes.c_int]
     L.satmi_resolution_debug_slot_base.argtypes = [ctypes.c_int64]
     L.satmi_resolution_debug_cand_bytes.argtypes = [ctypes.c_int64]
+    L.satmi_cdcl_last_stats.argtypes = [P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_int)]
     L.satmi_dp_last_stats.argtypes = [i64p, i64p, i64p, i64p, P(ctypes.c_int), P(ctypes.c_double)]
     L.satmi_cdcl_batch_host.argtypes = [ctypes.c_int, i32p, i32p, i32p, ctypes.c_int64, ctypes.c_int64,
                                         ctypes.c_double, i32p, i32p, i32p, ctypes.c_int, i64p,

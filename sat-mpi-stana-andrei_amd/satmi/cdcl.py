@@ -70,3 +70,15 @@ def cdcl_solve(formula, time_limit=0.0, learn_cap=1 << 24):
         raise KeyError("analyze_conflict reached an unassigned variable (the reference raises KeyError here)")
     raise CdclLimit(f"CDCL stopped after {r['stats']['iterations']} iterations "
                     f"({'arena full' if r['status'] == CDCL_FULL else 'time or iteration limit'})")
+
+
+def last_stats():
+    """The calling thread's last CDCL launch: span (s, device wall clock), busy
+    wave-time (s) and resident waves; utilisation = busy / (resident x span)."""
+    import ctypes
+    L = _capi.load()
+    span, busy, res = ctypes.c_double(0.0), ctypes.c_double(0.0), ctypes.c_int(0)
+    _capi.check(L.satmi_cdcl_last_stats(ctypes.byref(span), ctypes.byref(busy), ctypes.byref(res)),
+                "satmi_cdcl_last_stats")
+    util = busy.value / (res.value * span.value) if res.value and span.value > 0 else None
+    return {"span_s": span.value, "busy_wave_s": busy.value, "resident_waves": res.value, "wave_utilisation": util}
