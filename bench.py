@@ -221,7 +221,7 @@ def load_profile(name, key):
 
 
 def kernel_src_sha(kernel="dpll"):
-    src = {"dpll": "dpll_scan.hip", "cdcl": "cdcl.hip"}[kernel]
+    src = {"dpll": "dpll_scan.hip", "cdcl": "cdcl.hip", "res": "resolution.hip", "dp": "dp.hip"}[kernel]
     with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", src), "rb") as fh:
         return hashlib.sha256(fh.read()).hexdigest()[:16]
 
@@ -502,56 +502,55 @@ def run_dpll(args, world, rank, local):
     return out, host
 
 
-def dp_roofline(stats, cus, clock_hz):
-    """Davis-Putnam (php-dp): the subsumption filter dominates (dp_subsume_tiled_kernel,
-    one lane per new clause, candidate keys broadcast from LDS).  Its binding
-    resource is the LDS issue pipe: one ds_read of a K-word key serves the 256
-    lanes of a workgroup, so a CU retires at most 64 / K subset tests per
-    cycle (64 lanes x one key word per LDS instruction per cycle).  achieved =
-    subset tests performed / the filter's device time (HIP events)."""
+DP_MIN_KERNEL_US = 0.64   # shortest DP kernel in the r04 kernel trace (a launch with nothing to do)
+
+
+def dp_roofline(stats, solves_per_s):
+    """Davis-Putnam (php-dp): a solve is a chain of dependent kernel launches
+    (csrc/dp.hip: DP_LAUNCHES_PER_STEP per elimination step, 30 steps for
+    PHP(6,5)) whose sizes live on the device, replayed from a HIP graph; most
+    steps are small, so the chain's latency binds, not a pipe or HBM.
+    achieved = launches completed per second; peak = one launch per the
+    shortest kernel duration measured in the kernel trace
+    (profiles/r04/dp_kernel_stats.txt: a launch with no work); device_ms = the
+    steps' device time (HIP events) per solve."""
     if not stats:
         return None
-    tests = sum(s["subset_tests"] for s in stats) / len(stats)
-    ms = sum(s["subsume_ms"] for s in stats) / len(stats)
-    K = stats[-1]["words"]
-    if ms <= 0 or K <= 0:
-        return None
-    ach = tests / (ms * 1e-3)
-    peak = cus * clock_hz * 64.0 / K
-    return {"bound": "lds-issue", "achieved": ach, "peak": peak, "unit": "subset-tests/s", "frac": ach / peak,
-            "traffic": None, "kernel": "dp_subsume_tiled_kernel", "kernel_ms_per_step": ms,
-            "subset_tests_per_step": tests, "new_clauses_per_step": sum(s["new_clauses"] for s in stats) / len(stats),
-            "key_words": K, "clock_hz": clock_hz}
+    launches = sum(s["launches"] for s in stats) / len(stats)
+    dms = sum(s["device_ms"] for s in stats) / len(stats)
+    ach = launches * solves_per_s
+    peak = 1e6 / DP_MIN_KERNEL_US
+    return {"bound": "launch-latency", "achieved": ach, "peak": peak, "unit": "launches/s", "frac": ach / peak,
+            "traffic": None, "kernel": "dp step chain (9 kernels per elimination step)",
+            "launches_per_solve": launches, "device_ms_per_solve": dms,
+            "us_per_launch": dms * 1e3 / launches if launches else None,
+            "subset_tests_per_solve": sum(s["subset_tests"] for s in stats) / len(stats),
+            "new_clauses_per_solve": sum(s["new_clauses"] for s in stats) / len(stats), "key_words": stats[-1]["words"]}
 
 
 def saturation_roofline(stats, nvars):
-    """Resolution (php-res): the dominant of its two kernels per step, timed by
-    HIP events on the library's stream (satmi_resolution_last_stats).  Claim
-    kernel (hash dedup), K = 2 x 64-bit words per clause key for <= 64
-    variables: with <= 31 variables the table holds packed one-word keys
-    (csrc/resolution.hip pack_key) -- per candidate its key read (8K B), one
-    slot read + CAS (16 B), its flag written (8 B); beyond, per candidate its
-    key (8K B), one slot read + CAS (16 B), the occupant's key compared (8K B),
-    flag + slot written (16 B).  Pair kernel: per pair key i read (8K B), per
-    candidate its key written (8K B)."""
+    """Resolution (php-res, <= 31 variables): one fused pass kernel per
+    saturation pass (csrc/resolution.hip res_pass_packed_kernel: pair
+    classification + claims in a table that stays in L2/MALL), timed per step
+    by HIP events.  Its binding pipe comes from the SQ passes of
+    tools/pmc_workload.sh (profiles/sq_issue.json "php-res_B1", per step): the
+    issue roofline over this run's live kernel time; the HBM bytes per step
+    (FETCH x2 + WRITE, the same passes) beside it -- a small fraction of HBM:
+    the table and the keys are cache-resident."""
     if not stats:
         return None
-    K = 2   # PHP(4,3): 12 variables -> one word per sign
-    packed = nvars <= 31
-    cand = sum(s["candidates"] for s in stats) / len(stats)
-    pairs = sum(s["pairs"] for s in stats) / len(stats)
-    cms = sum(s["claim_ms"] for s in stats) / len(stats)
     pms = sum(s["pair_ms"] for s in stats) / len(stats)
-    claim_b = cand * (8 * K + 24) if packed else cand * (16 * K + 32)
-    pair_b = pairs * 8 * K + cand * 8 * K
-    name, b, ms = ("ht_cand_packed_kernel (hash claims)" if packed else "ht_cand_kernel (hash claims)",
-                   claim_b, cms) if cms >= pms else ("res_pairs_kernel", pair_b, pms)
-    ach = b / (ms * 1e-3) / 1e9
-    pmc = load_profile("pmc_traffic.json", "php-res_" + name.split()[0])
-    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "traffic": pmc.get("hbm_bytes_per_step") if pmc else None, "kernel": name,
-            "kernel_ms_per_step": ms, "algorithmic_bytes_per_step": b,
-            "candidates_per_step": cand, "pairs_per_step": pairs, "pair_ms_per_step": pms, "claim_ms_per_step": cms}
+    roof = issue_roofline("php-res", 1, pms, kernel="res")
+    if roof is None:
+        return None
+    e = load_profile("sq_issue.json", "php-res_B1") or {}
+    roof.update({"kernel": "res_pass_packed_kernel (fused pairs + claims)", "kernel_ms_per_step": pms,
+                 "pairs_per_step": sum(s["pairs"] for s in stats) / len(stats),
+                 "candidates_per_step": sum(s["candidates"] for s in stats) / len(stats),
+                 "hbm_bytes_per_step": e.get("hbm_bytes_corrected"),
+                 "hbm_frac": (e["hbm_bytes_corrected"] / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                 if e.get("hbm_bytes_corrected") else None})
+    return roof
 
 
 def run_saturation(args, world, rank, local):
@@ -618,7 +617,7 @@ def run_saturation(args, world, rank, local):
                       "preset": args.workload, "parallelism": f"replicas x{world}", "concurrent_solves": T},
            "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
            "roofline": saturation_roofline(stats, len({abs(l) for c in f for l in c})) if args.workload == "php-res" else
-           dp_roofline(stats, torch.cuda.get_device_properties(local).multi_processor_count, SHADER_CLOCK_HZ)}
+           dp_roofline(stats, done * world / elapsed)}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:
         # the oracle on the same formula: checked against the GPU, then replicas

@@ -169,12 +169,13 @@ int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_li
                   int trace_cap, int32_t *h_steps, int32_t *h_rec_lits, int64_t rec_lit_cap,
                   int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_step_off, int rec_step_cap);
 
-/* Work of the calling thread's last satmi_dp_host call's subsumption filter (REF.py:122-125):
- * elimination steps, subset tests performed, new (non-tautological) clauses
- * filtered, bytes of candidate keys, key words per clause, and the filter's
- * device time (HIP events on its stream), for rooflines. */
-int satmi_dp_last_stats(int64_t *steps, int64_t *subset_tests, int64_t *new_clauses, int64_t *candidate_bytes,
-                        int *words, double *subsume_ms);
+/* Work of the calling thread's last satmi_dp_host call: elimination steps,
+ * subset tests performed by the unique_new filter (REF.py:122-125), new
+ * (non-tautological) resolvents, kernel launches enqueued for the steps, key
+ * words per clause, and the device time of the step batches (HIP events on its
+ * stream), for rooflines. */
+int satmi_dp_last_stats(int64_t *steps, int64_t *subset_tests, int64_t *new_clauses, int64_t *launches,
+                        int *words, double *device_ms);
 
 /* Free the idle device workspaces that satmi_dp_host / satmi_resolution_host
  * keep between calls (buffers only grow while kept); calls in flight keep theirs. */

@@ -72,6 +72,7 @@ enum : int32_t { OVF_PAIRS = 1, OVF_NCL = 2, OVF_ARENA = 4, OVF_XS = 8 };
 
 constexpr uint64_t DP_EMPTY = ~0ull;
 constexpr int DP_STRIPES = 64;
+constexpr int DP_LAUNCHES_PER_STEP = 9;   // pop_split, pairs, hash, gather, remtest, survlist, survtest, kept, assemble
 
 // The solve's state, on the device.  Host writes it once per solve (and on a
 // resume); kernels read sizes from it and one thread of the single-workgroup
@@ -965,8 +966,8 @@ struct Gen {   // one generation's per-clause arrays
 
 // Work and device time of the last satmi_dp_host call, for bench.py's roofline.
 struct DpStats {
-    int64_t steps = 0, tests = 0, new_clauses = 0, candidates_bytes = 0;
-    double subsume_ms = 0.0;
+    int64_t steps = 0, tests = 0, new_clauses = 0, launches = 0;
+    double device_ms = 0.0;
     int words = 0;
 };
 thread_local DpStats g_dp_stats;   // the calling thread's last call
@@ -1283,7 +1284,7 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         }
         return &Wk.ev[2 * nev++];
     };
-    // one elimination step: eight launches, sizes on the device
+    // one elimination step: DP_LAUNCHES_PER_STEP launches, sizes on the device
     const auto enqueue_step = [&](const DpArgs &a) -> int {
         const int gp = (int)std::min<int64_t>(1024, (a.pair_cap + 255) / 256);
         const int gc = (int)std::min<int64_t>(2048, (a.ncl_cap + ASM_WAVES - 1) / ASM_WAVES);
@@ -1358,6 +1359,7 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         }
         SATMI_HIP(hipEventRecord(ev[1], s));
         enqueued += batch;
+        g_dp_stats.launches += (int64_t)batch * DP_LAUNCHES_PER_STEP;
         SATMI_HIP(hipMemcpyAsync(Wk.pin, Wk.state.p, sizeof(DpState), hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
         if (st.set_ovf) {
@@ -1429,7 +1431,7 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     g_dp_stats.new_clauses = st.new_total;
     for (size_t i = 0; i < nev; ++i) {   // the stream has drained
         float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, Wk.ev[2 * i], Wk.ev[2 * i + 1]) == hipSuccess) g_dp_stats.subsume_ms += ms;
+        if (hipEventElapsedTime(&ms, Wk.ev[2 * i], Wk.ev[2 * i + 1]) == hipSuccess) g_dp_stats.device_ms += ms;
     }
     *h_result = st.result;
     *h_steps = steps;
@@ -1438,13 +1440,13 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
 }
 
 extern "C" int satmi_dp_last_stats(int64_t *steps, int64_t *subset_tests, int64_t *new_clauses,
-                                   int64_t *candidate_bytes, int *words, double *subsume_ms) {
+                                   int64_t *launches, int *words, double *device_ms) {
     if (steps) *steps = g_dp_stats.steps;
     if (subset_tests) *subset_tests = g_dp_stats.tests;
     if (new_clauses) *new_clauses = g_dp_stats.new_clauses;
-    if (candidate_bytes) *candidate_bytes = g_dp_stats.candidates_bytes;
+    if (launches) *launches = g_dp_stats.launches;
     if (words) *words = g_dp_stats.words;
-    if (subsume_ms) *subsume_ms = g_dp_stats.subsume_ms;
+    if (device_ms) *device_ms = g_dp_stats.device_ms;
     return SATMI_OK;
 }
 

@@ -404,6 +404,17 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const bool unit = sv == 1u;
             const uint64_t um = __ballot(unit);
             const int nun = __popcll(um);
+#ifdef SATMI_EXP_UNIT1
+            if (nun <= 1) {   // one unit clause (or none): snapshot index 0, no duplicate to drop
+                if (unit) {
+                    const uint32_t code = unit_code<K>(w, x);
+                    S.snap[0] = (C)code;
+                    ts_stamp(S, code >> 1, stamp(ep, 0u));
+                }
+                wave_sync();
+                return nun;
+            }
+#endif
             if (__builtin_expect(nun <= FAST_UNITS, 1)) {
                 // a clause reached from two batch literals is one snapshot entry
                 bool dup = false;
@@ -579,11 +590,22 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             const bool first = S.ts[v] == stamp(bep, (uint32_t)k);
 #endif
             const uint64_t mk = __ballot(first);
+#ifdef SATMI_EXP_PREDASSIGN
+            {   // predicated: the other lanes write their own (consumed) snapshot entry and the
+                // pinned codes' own values (no exec-mask region)
+                const uint32_t ts_slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mk, (uint32_t)tl));
+                C *dst = first ? S.trail + ts_slot : S.snap + (k < nu ? k : 0);
+                *dst = (C)code;   // (a lane past nu rewrites entry 0's own value)
+                lv_assign(S.lv, first ? code : CODE_DUMMY);
+            }
+#else
             if (first) {   // trail slot: tl + the first entries on lower lanes (k order)
                 S.trail[__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mk, (uint32_t)tl))] = (C)code;
                 lv_assign(S.lv, code);
             }
+#endif
 #ifdef SATMI_DUP_ASSIGN
             {
                 const uint32_t cd = first ? code : CODE_DUMMY;

@@ -52,14 +52,16 @@ def eliminate(formula, step_limit=0, clause_limit=0, time_limit=0.0, record=Fals
 
 
 def last_stats():
-    """Work of the last eliminate() call's subsumption filter (satmi_dp_last_stats)."""
+    """Work of the last eliminate() call in this thread (satmi_dp_last_stats):
+    steps, subset tests, new resolvents, kernel launches, key words and the
+    device time of the elimination steps (ms)."""
     v = [ctypes.c_int64(0) for _ in range(4)]
     w = ctypes.c_int(0)
     ms = ctypes.c_double(0.0)
     _capi.check(_capi.load().satmi_dp_last_stats(*(ctypes.byref(x) for x in v), ctypes.byref(w), ctypes.byref(ms)),
                 "satmi_dp_last_stats")
     return {"steps": v[0].value, "subset_tests": v[1].value, "new_clauses": v[2].value,
-            "candidate_bytes": v[3].value, "words": w.value, "subsume_ms": ms.value}
+            "launches": v[3].value, "words": w.value, "device_ms": ms.value}
 
 
 def davis_putnam_solve(formula, time_limit=0.0):

@@ -12,13 +12,13 @@ export TMPDIR=/tmp
 SUM="$OUT/pmc_$WL.txt"
 : > "$SUM"
 i=0
-GROUPS=${PMC_GROUPS:-"sq1 sq2 tcc fetch write"}
+PASSES=${PMC_GROUPS:-"sq1 sq2 tcc fetch write"}
 declare -A G=(
   [sq1]="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"
   [sq2]="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
   [tcc]="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_ATOMIC_sum"
   [fetch]="FETCH_SIZE" [write]="WRITE_SIZE")
-for gname in $GROUPS; do
+for gname in $PASSES; do
   grp=${G[$gname]}
   i=$((i + 1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$ROOT/$OUT/p$i" -o p$i \

@@ -1,7 +1,12 @@
 """Issue-pipe roofline inputs of a kernel from tools/pmc_workload.sh's SQ passes
 (sq1 + sq2), stored in profiles/sq_issue.json for bench.py's issue_roofline().
 
-    python tools/sq_issue_entry.py gpurun_out/<tag> <workload> <kernel substring> <key> <src> [keep dir]
+    python tools/sq_issue_entry.py gpurun_out/<tag> <workload> <kernel substring> <key> <src> [keep dir] [--per-step]
+
+--per-step: a step of the workload is several launches (resolution: one pass
+kernel per saturation pass), so the counts are divided by the bench line's
+steps + warmup instead of by the dispatches, and the live time is the line's
+roofline.kernel_ms_per_step.
 
 Per launch (the counters summed over the kernel's dispatches / dispatches):
 wave-instructions per pipe (SQ_INSTS_*), LDS-array cycles (SQ_LDS_IDX_ACTIVE,
@@ -23,8 +28,10 @@ CUS, SIMDS, XCDS = 256, 1024, 8
 
 
 def main():
-    src, wl, kname, key, ksrc = sys.argv[1:6]
-    keep = sys.argv[6] if len(sys.argv) > 6 else None
+    argv = [a for a in sys.argv[1:] if a != "--per-step"]
+    per_step = "--per-step" in sys.argv
+    src, wl, kname, key, ksrc = argv[:5]
+    keep = argv[5] if len(argv) > 5 else None
     vals, ndisp = {}, {}
     section = None
     with open(os.path.join(src, f"pmc_{wl}.txt")) as fh:
@@ -39,14 +46,20 @@ def main():
     nd = ndisp["SQ_INSTS_VALU"]
     with open(os.path.join(src, "p1.json")) as fh:
         bench = json.loads(fh.read().strip().splitlines()[-1])
-    kms = bench.get("kernel_ms") or bench["roofline"]["kernel_ms"]
-    per = lambda k: vals[k] / ndisp[k]   # noqa: E731
+    if per_step:
+        kms = bench["roofline"]["kernel_ms_per_step"]
+        nunits = bench["steps"] + bench["warmup"]
+        per = lambda k: vals[k] / nunits   # noqa: E731
+    else:
+        kms = bench.get("kernel_ms") or bench["roofline"]["kernel_ms"]
+        per = lambda k: vals[k] / ndisp[k]   # noqa: E731
     clock = per("GRBM_GUI_ACTIVE") / XCDS / (kms * 1e-3)
     cyc = clock * kms * 1e-3
     with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", ksrc), "rb") as fh:
         sha = hashlib.sha256(fh.read()).hexdigest()[:16]
     entry = {
         "kernel": kname, "kernel_src_sha256_16": sha, "dispatches": nd, "profiled_kernel_ms": kms,
+        "per": "step" if per_step else "launch",
         "effective_clock_hz": clock,
         "valu_insts": per("SQ_INSTS_VALU"), "salu_insts": per("SQ_INSTS_SALU"), "lds_insts": per("SQ_INSTS_LDS"),
         "branch_insts": per("SQ_INSTS_BRANCH"), "vmem_rd_insts": per("SQ_INSTS_VMEM_RD"),
@@ -72,6 +85,14 @@ def main():
         os.makedirs(os.path.join(ROOT, keep), exist_ok=True)
         shutil.copy(os.path.join(src, f"pmc_{wl}.txt"), os.path.join(ROOT, keep, f"pmc_{wl}.txt"))
         shutil.copy(os.path.join(src, "p1.json"), os.path.join(ROOT, keep, f"pmc_{wl}_bench.json"))
+    # HBM bytes from the FETCH_SIZE / WRITE_SIZE passes when present (KB units;
+    # FETCH x2 per MI355X_MICROARCH.md's gfx950 correction, raw beside it)
+    if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+        entry["fetch_bytes_raw"] = per("FETCH_SIZE") * 1024
+        entry["hbm_bytes_corrected"] = 2 * per("FETCH_SIZE") * 1024 + per("WRITE_SIZE") * 1024
+        table[key] = entry
+        with open(OUT, "w") as fh:
+            json.dump(table, fh, indent=1, sort_keys=True)
     print(json.dumps({key: entry}, indent=1))
 
 
