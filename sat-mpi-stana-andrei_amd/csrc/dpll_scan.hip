@@ -74,19 +74,6 @@ enum { PH_STAGE = 0, PH_ASSIGN = 1, PH_UNITS = 2, PH_CONFLICT = 3, PH_COUNTS = 4
 
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 
-// Attribution builds only (`make variant VFLAGS=-DSATMI_DUP_<KIND>`, never the
-// product): every LDS access of one kind is issued a second time with an
-// effect-free operand (OR / ADD of an opaque zero, MIN of all ones, MAX of 0),
-// so the search is unchanged and the rise of SQ_LDS_BANK_CONFLICT over the
-// plain build is that kind's conflict cycles.  Kinds: GATHER (literal-state
-// byte gathers), CNT (counting-pass atomics), TS (snapshot stamp atomics),
-// CLS (touched-clause word reads of the incremental rounds), ASSIGN (the
-// batch assignment's stamp reads and state stores).
-__device__ __forceinline__ uint32_t opaque_zero() {
-    uint32_t z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    return z;
-}
 
 // Literal state byte lv[code] (code = v << 1 | negative): free 1, true 8,
 // false 0.  The sum of a clause's bytes: bits 0-2 = free occurrences (REF.py's
@@ -187,30 +174,10 @@ __device__ __forceinline__ void lv_clear(uint8_t *lv, uint32_t v) {
 }
 __device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return (lv[2 * v] & 1u) != 0u; }
 
-// The hot LDS accesses by kind (see SATMI_DUP_* above).
-template <int K, typename C>
-__device__ __forceinline__ uint32_t lv_get(const SLds<K, C> &S, uint32_t code) {
-    uint32_t x = S.lv[code];
-#ifdef SATMI_DUP_GATHER
-    x |= (uint32_t)((const volatile uint8_t *)S.lv)[code] & opaque_zero();
-#endif
-    return x;
-}
-template <int K, typename C>
-__device__ __forceinline__ void ts_stamp(const SLds<K, C> &S, uint32_t v, uint32_t st) {
-    atomicMax(&S.ts[v], st);
-#ifdef SATMI_DUP_TS
-    atomicMax(&S.ts[v], st & opaque_zero());
-#endif
-}
-template <int K, typename C>
-__device__ __forceinline__ typename Pack<K>::W cls_at(const SLds<K, C> &S, uint32_t c) {
-    typename Pack<K>::W w = S.cls[c];
-#ifdef SATMI_DUP_CLS
-    w |= ((const volatile typename Pack<K>::W *)S.cls)[c] & (typename Pack<K>::W)opaque_zero();
-#endif
-    return w;
-}
+// The hot LDS accesses by kind: the product forms, or (attribution builds,
+// never the product) each issued twice -- see dpll_scan_access.h.
+#include "dpll_scan_access.h"
+
 
 // Apply f(c, w, x) to every clause c (w its packed word, x[j] the state byte of
 // its slot j), one 64-clause chunk per lane step; the loads of U chunks are
@@ -404,17 +371,6 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const bool unit = sv == 1u;
             const uint64_t um = __ballot(unit);
             const int nun = __popcll(um);
-#ifdef SATMI_EXP_UNIT1
-            if (nun <= 1) {   // one unit clause (or none): snapshot index 0, no duplicate to drop
-                if (unit) {
-                    const uint32_t code = unit_code<K>(w, x);
-                    S.snap[0] = (C)code;
-                    ts_stamp(S, code >> 1, stamp(ep, 0u));
-                }
-                wave_sync();
-                return nun;
-            }
-#endif
             if (__builtin_expect(nun <= FAST_UNITS, 1)) {
                 // a clause reached from two batch literals is one snapshot entry
                 bool dup = false;
@@ -583,35 +539,14 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             const uint32_t code = (uint32_t)S.snap[k < nu ? k : 0];
             const uint32_t v = code >> 1;
             // (one compare: its ballot folds into the v_cmp)
-#ifdef SATMI_DUP_ASSIGN
-            const bool first = (S.ts[v] | (((const volatile uint32_t *)S.ts)[v] & opaque_zero())) ==
-                               stamp(bep, (uint32_t)k);
-#else
-            const bool first = S.ts[v] == stamp(bep, (uint32_t)k);
-#endif
+            const bool first = ts_first(S, v) == stamp(bep, (uint32_t)k);
             const uint64_t mk = __ballot(first);
-#ifdef SATMI_EXP_PREDASSIGN
-            {   // predicated: the other lanes write their own (consumed) snapshot entry and the
-                // pinned codes' own values (no exec-mask region)
-                const uint32_t ts_slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mk, (uint32_t)tl));
-                C *dst = first ? S.trail + ts_slot : S.snap + (k < nu ? k : 0);
-                *dst = (C)code;   // (a lane past nu rewrites entry 0's own value)
-                lv_assign(S.lv, first ? code : CODE_DUMMY);
-            }
-#else
             if (first) {   // trail slot: tl + the first entries on lower lanes (k order)
                 S.trail[__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mk, (uint32_t)tl))] = (C)code;
                 lv_assign(S.lv, code);
             }
-#endif
-#ifdef SATMI_DUP_ASSIGN
-            {
-                const uint32_t cd = first ? code : CODE_DUMMY;
-                *(volatile uint16_t *)(S.lv + (cd & ~1u)) = (uint16_t)((cd & 1u) ? (LV_TRUE << 8) : LV_TRUE);
-            }
-#endif
+            dup_assign_store(S, first, code);
             tl += __popcll(mk);
             k0 += 64;
         } while (k0 < nu);
@@ -666,9 +601,7 @@ __device__ int scan_counts(const SLds<K, C> &S, int mpad) {
             for (int j = 0; j < K; ++j) {
                 const uint32_t code = field<K>(w, j);
                 atomicAdd(&S.cnt[code], x[j]);
-#ifdef SATMI_DUP_CNT
-                atomicAdd(&S.cnt[code], opaque_zero());
-#endif
+                dup_count(S, code);
             }
         }
     });
