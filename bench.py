@@ -625,9 +625,12 @@ def run_saturation(args, world, rank, local):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         r = oracle.dp(f) if args.workload == "php-dp" else oracle.resolution(f, max_passes=npass)
-        w = 1 if args.workload == "php-dp" else sum(r["pass_new"])
-        if r["result"] != last["result"] or w != work(last):
-            raise SystemExit("bench: GPU and oracle disagree on the configs[3] workload")
+        # per pass (resolution: every pass's new-clause count) / per step (DP)
+        per = (lambda x: [x["steps"], list(x["vars"])]) if args.workload == "php-dp" else (lambda x: list(x["pass_new"]))   # noqa: E731
+        if r["result"] != last["result"] or per(r) != per(last):
+            raise SystemExit(f"bench: GPU and oracle disagree on the configs[3] workload: "
+                             f"{last['result']} {per(last)} vs {r['result']} {per(r)}")
+        out["oracle_check"] = {"result": r["result"], ("steps_vars" if args.workload == "php-dp" else "pass_new"): per(r)}
         hb = cnf.pack([f])
         pool, cores = cpu_pool("dp" if args.workload == "php-dp" else "res", hb.inst_clause_begin,
                                hb.clause_lit_begin, hb.lits, args.cpu_seconds, npass)
