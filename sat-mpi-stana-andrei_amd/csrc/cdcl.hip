@@ -15,12 +15,12 @@
 //   * activity / var_inc: IEEE double arithmetic in the reference's order
 //     (REF.py:355-357, :378), max() keeping the first maximal variable.
 // What runs across the wave's 64 lanes (everything else is lane 0):
-//   * propagate (REF.py:269-304): per false watch literal, the set's table is
-//     compacted into its iteration-order snapshot by ballots; the replacement
-//     watch of every snapshot clause (its first other literal that is free or
-//     true) is found one clause per lane; the first clause without one is the
-//     conflict; the snapshot's removals are dummy marks at known slots (no
-//     resize on discard), the adds go in order on lane 0 (they may create keys);
+//   * propagate (REF.py:269-304): the tables of all false watch literals are
+//     read as one stream in the reference's visiting order, one slot per lane;
+//     the replacement watch of every member (its first other literal that is
+//     free or true) is found in parallel; the first member without one is the
+//     conflict; the removals are dummy marks at known slots (no resize on
+//     discard), the adds go in order on lane 0 (they may create keys);
 //   * the all-assigned test (REF.py:257) over a bitmap of the variables that
 //     occur; select_variable's max over activities (REF.py:370-379);
 //     backtracking (REF.py:359-368); the model's dict order (a rank per stamp).
@@ -49,9 +49,9 @@ enum { CD_FALSE = 0, CD_TRUE = 1, CD_LIMIT = -1, CD_ERROR = -2, CD_FULL = -3 };
 
 // Per-wave arena layout (offsets in bytes), sized on the host for the batch.
 struct CdclLayout {
-    uint64_t coff, lits, val, ord, lev, ante, act, appears, klit, kidx, woff, wmask, wfill, wused, pool, snap, rep,
-        slot, scratch, bytes;
-    int64_t clause_cap, lit_cap, pool_cap, snap_cap;
+    uint64_t coff, lits, val, ord, lev, ante, act, appears, klit, kidx, woff, wmask, wfill, wused, pool, scratch,
+        bytes;
+    int64_t clause_cap, lit_cap, pool_cap;
     int32_t ncap;   // variables
     int32_t lcap;   // one learned-literal list in scratch: 2 x variables + the longest clause (repeats)
     // the per-variable and per-key arrays ([val, pool) of the arena) and the
@@ -87,15 +87,17 @@ struct St {   // views into one wave's arena
     int32_t *klit, *kidx;
     int64_t *woff;
     int32_t *wmask, *wfill, *wused;
-    int32_t *pool, *snap, *rep, *slot, *scratch;
+    int32_t *pool, *scratch;
 #ifdef SATMI_CDCL_PHASES
-    uint64_t *clk;   // diagnostic build: per-phase shader clocks (lane 0), [7] = last stamp
+    uint64_t *clk;   // diagnostic build: per-phase shader clocks and counts (lane 0), [7] = last stamp
 #endif
 };
 
-// Diagnostic build only (make variant VFLAGS=-DSATMI_CDCL_PHASES): per-phase
-// clocks of a solve written over stats[4..7] (snapshot, replacement watches,
-// watch-list moves, everything between propagate calls).
+// Diagnostic build only (make variant VFLAGS=-DSATMI_CDCL_PHASES, read by
+// tools/cdcl_probe.py): per-phase clocks of a solve written over stats[4..7]
+// (snapshot, replacement watches, watch-list moves, everything between
+// propagate calls) and counts over stats[1..3] (moves, snapshot entries, false
+// watch lists visited).
 #ifdef SATMI_CDCL_PHASES
 #define CDCL_CLK(S, i)                                             \
     do {                                                           \
@@ -163,6 +165,11 @@ __device__ void ws_resize(const CdclArgs &A, const St &S, Seq &q, int k, int64_t
     if (newsize == WS_MINSIZE && mask == WS_MINSIZE - 1 && S.wfill[k] == S.wused[k]) return;
     int64_t off;
     if (!ws_alloc(A, q, newsize, &off)) return;
+#ifdef SATMI_CDCL_PHASES
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    S.clk[10] += 1;
+    S.clk[11] += (uint64_t)S.wused[k];
+#endif
     int32_t *nt = S.pool + off, *ot = S.pool + S.woff[k];
     for (int64_t i = 0; i < newsize; ++i) nt[i] = WS_EMPTY;
     for (int64_t i = 0; i <= mask; ++i)
@@ -170,6 +177,9 @@ __device__ void ws_resize(const CdclArgs &A, const St &S, Seq &q, int k, int64_t
     S.woff[k] = off;
     S.wmask[k] = (int32_t)(newsize - 1);
     S.wfill[k] = S.wused[k];
+#ifdef SATMI_CDCL_PHASES
+    S.clk[9] += __builtin_amdgcn_s_memtime() - t0;
+#endif
 }
 
 // set_add_entry(so, key, hash = key - 1)  (lane 0)
@@ -239,8 +249,15 @@ __device__ int key_of(const CdclArgs &A, const St &S, Seq &q, int lit) {
 }
 
 __device__ void watch_add(const CdclArgs &A, const St &S, Seq &q, int lit, int64_t idx) {
+#ifdef SATMI_CDCL_PHASES
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
     const int k = key_of(A, S, q, lit);
     if (k >= 0 && !q.full) ws_add(A, S, q, k, (int32_t)(idx + 1));
+#ifdef SATMI_CDCL_PHASES
+    S.clk[8] += __builtin_amdgcn_s_memtime() - t0;   // (lane 0)
+    S.clk[12] += 1;
+#endif
 }
 
 __device__ __forceinline__ bool lit_false(const St &S, int lit) {
@@ -272,96 +289,151 @@ __device__ void sync_seq(Seq &q) {
 // (The reference's unit branch, REF.py:290-291 / :297-304, needs a watched
 // clause of length 1; watched clauses are longer than 1 (REF.py:235, :351),
 // so its pass ends either at a conflict or with `unit is None`.)
+//
+// Nothing the pass does changes what it reads: it assigns nothing, a
+// replacement watch is never a false literal (so every add goes to the table
+// of a literal the pass does not visit) and a removal only marks a slot of the
+// visited table itself.  So the tables of all false watch literals are read as
+// ONE stream -- keys in dict order, each table in slot order, which is the
+// order REF.py:274-276 visits them -- in windows of up to 256 slots; every
+// member of a window looks for its replacement watch at the same time; the
+// first member without one (stream order) is the conflict (REF.py:292-293),
+// and the members before it move: dummies at their slots, the adds in stream
+// order on lane 0 (they may create keys and resize tables).  A launch's long
+// solves are latency-bound chains of dependent memory reads, and one window
+// covers the false lists of a typical pass at once.
+constexpr int CDCL_LITS_AHEAD = 4;   // a member's first literals read at once
+
 __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
     const int ln = lane_id();
-    const uint64_t lt = lanemask_lt();
     CDCL_CLK(S, 3);
     const int nk0 = q.nk;   // list(self.watch_list): keys created during the pass are not visited
     for (int k0 = 0; k0 < nk0; k0 += 64) {
         const int kk = k0 + ln;
         const bool fl = kk < nk0 && lit_false(S, S.klit[kk]);
-        uint64_t fm = __ballot(fl);
-        while (fm) {
-            const int ki = k0 + __builtin_ctzll(fm);
-            fm &= fm - 1;
-            const int lit = S.klit[ki];
-            // snapshot of the set in iteration order (table slot order), with
-            // slots, taken a window of 64, then 256 slots at a time: the replacement
-            // watches of a window's members are found before the next window
-            // is read, so a conflict ends the snapshot too (REF.py's loop
-            // returns at the first clause without a replacement; the members
-            // after it are never visited)
-            const int32_t *t = S.pool + S.woff[ki];
-            const int32_t mask = S.wmask[ki];
-            int n = 0;
-            int64_t conflict = -1;
-            int upto = -1;   // snapshot entries whose watch moves (before the conflict)
-            for (int i0 = 0, nch = 1; i0 <= mask && upto < 0; i0 += 64 * nch, nch = 4) {
-                const int n0 = n;
-                int32_t xs[4];   // up to four table reads in flight (the first window: one)
+        const int size = fl ? S.wmask[kk] + 1 : 0;
+        const int incl = wave_incl_scan(size);
+        const int total = lane63(incl), excl = incl - size;
+        const uint64_t fm = __ballot(fl);
+#ifdef SATMI_CDCL_PHASES
+        if (ln == 0) S.clk[6] += (uint64_t)__popcll(fm);
+#endif
+        for (int g0 = 0, nch; g0 < total; g0 += 64 * nch) {
+            nch = min(4, (total - g0 + 63) >> 6);   // one window when the stream fits 256 slots
+            // the stream slot g of (u, lane): its key (the last false key whose
+            // table starts at or before g) and the slot in that table
+            int own[4], ex[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) own[u] = ex[u] = 0;
+            for (uint64_t m = fm; m; m &= m - 1) {
+                const int bl = __builtin_ctzll(m);
+                const int eb = __builtin_amdgcn_readlane(excl, bl);
+                if (eb >= g0 + 64 * nch) break;   // keys past the window
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int i = i0 + 64 * u + ln;
-                    xs[u] = (u < nch && i <= mask) ? t[i] : WS_EMPTY;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int32_t x = xs[u];
-                    const bool act = x != WS_EMPTY && x != WS_DUMMY;
-                    const uint64_t am = __ballot(act);
-                    if (act) {
-                        const int p = n + __popcll(am & lt);
-                        S.snap[p] = x - 1;
-                        S.slot[p] = i0 + 64 * u + ln;
+                    if (u < nch) {
+                        const bool after = g0 + 64 * u + ln >= eb;
+                        own[u] = after ? bl : own[u];
+                        ex[u] = after ? eb : ex[u];
                     }
-                    n += __popcll(am);
                 }
-                wave_sync();
-                CDCL_CLK(S, 0);
-                // replacement watch per snapshot clause, one clause per lane
-                for (int p0 = n0; p0 < n; p0 += 64) {
-                    const int p = p0 + ln;
-                    int r = 0;
-                    bool none = false;
-                    if (p < n) {
-                        const int64_t c = S.snap[p];
-                        const int64_t jb = S.coff[c], je = S.coff[c + 1];
-                        for (int64_t j = jb; j < je; ++j) {
-                            const int o = S.lits[j];
-                            if (o == lit) continue;
-                            const int8_t v = S.val[iabs(o)];
-                            if (v < 0 || (o > 0) == (v != 0)) {
-                                r = o;
-                                break;
-                            }
+            }
+            int32_t x[4], lit[4];
+            int64_t at[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {   // up to four table reads in flight
+                const int g = g0 + 64 * u + ln;
+                const bool in = u < nch && g < total;
+                const int k = k0 + own[u];
+                at[u] = in ? S.woff[k] + (g - ex[u]) : 0;
+                lit[u] = in ? S.klit[k] : 0;
+                x[u] = in ? S.pool[at[u]] : WS_EMPTY;
+            }
+            bool act[4];
+            int64_t jb[4], je[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                act[u] = x[u] != WS_EMPTY && x[u] != WS_DUMMY;
+                jb[u] = act[u] ? S.coff[x[u] - 1] : 0;
+                je[u] = act[u] ? S.coff[x[u]] : 0;
+            }
+            CDCL_CLK(S, 0);
+            // replacement watch: the clause's first literal other than lit that
+            // is free or true (REF.py:279-286); the first CDCL_LITS_AHEAD of
+            // every member are read together
+            int r[4];
+            int o[4][CDCL_LITS_AHEAD];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int t = 0; t < CDCL_LITS_AHEAD; ++t) o[u][t] = jb[u] + t < je[u] ? S.lits[jb[u] + t] : lit[u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                r[u] = 0;
+#pragma unroll
+                for (int t = 0; t < CDCL_LITS_AHEAD; ++t) {
+                    const int ot = o[u][t];
+                    const int8_t v = S.val[iabs(ot)];
+                    r[u] = (r[u] == 0 && ot != lit[u] && (v < 0 || (ot > 0) == (v != 0))) ? ot : r[u];
+                }
+                if (act[u] && r[u] == 0) {   // longer clauses: the rest one literal at a time
+                    for (int64_t j = jb[u] + CDCL_LITS_AHEAD; j < je[u]; ++j) {
+                        const int ot = S.lits[j];
+                        if (ot == lit[u]) continue;
+                        const int8_t v = S.val[iabs(ot)];
+                        if (v < 0 || (ot > 0) == (v != 0)) {
+                            r[u] = ot;
+                            break;
                         }
-                        none = r == 0;
-                        S.rep[p] = r;
-                    }
-                    const uint64_t nm = __ballot(none);
-                    if (nm) {
-                        upto = p0 + __builtin_ctzll(nm);
-                        conflict = S.snap[upto];
-                        break;
                     }
                 }
-                CDCL_CLK(S, 1);
             }
-            if (upto < 0) upto = n;
-            wave_sync();
-            conflict = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)conflict) |
-                       ((int64_t)__builtin_amdgcn_readfirstlane((int)(conflict >> 32)) << 32);
-            upto = __builtin_amdgcn_readfirstlane(upto);
+            // the first member without a replacement, in stream order (u, lane)
+            int cu = 4, cl = 64;
+            int64_t conflict = -1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t nm = __ballot(act[u] && r[u] == 0);
+                if (cu == 4 && nm) {
+                    cu = u;
+                    cl = __builtin_ctzll(nm);
+                    conflict = (int64_t)__builtin_amdgcn_readlane(x[u], cl) - 1;
+                }
+            }
             CDCL_CLK(S, 1);
-            // self.watch_list[lit].remove(idx): dummies at the snapshot's slots
-            int32_t *tw = S.pool + S.woff[ki];
-            for (int p = ln; p < upto; p += 64) tw[S.slot[p]] = WS_DUMMY;
-            if (ln == 0) {
-                S.wused[ki] -= upto;
-                // self.watch_list[other_lit].add(idx), in snapshot order
-                for (int p = 0; p < upto && !q.full; ++p) watch_add(A, S, q, S.rep[p], S.snap[p]);
+            // the moves: self.watch_list[lit].remove(idx) (a dummy at its slot),
+            // self.watch_list[other_lit].add(idx) in stream order
+            int nmv = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool mv = act[u] && r[u] != 0 && (u < cu || (u == cu && ln < cl));
+                if (mv) S.pool[at[u]] = WS_DUMMY;
+                uint64_t mm = __ballot(mv);
+                nmv += __popcll(mm);
+                for (; mm; mm &= mm - 1) {
+                    const int l = __builtin_ctzll(mm);
+                    const int rl = __builtin_amdgcn_readlane(r[u], l);
+                    const int cx = __builtin_amdgcn_readlane(x[u], l);
+                    const int kl = k0 + __builtin_amdgcn_readlane(own[u], l);
+                    if (ln == 0) {
+                        S.wused[kl] -= 1;
+                        if (!q.full) watch_add(A, S, q, rl, (int64_t)cx - 1);
+                    }
+                }
             }
-            sync_seq(q);
+#ifdef SATMI_CDCL_PHASES
+            {   // diagnostic counts: moves, members read
+                int na = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) na += __popcll(__ballot(act[u]));
+                if (ln == 0) {
+                    S.clk[4] += (uint64_t)nmv;
+                    S.clk[5] += (uint64_t)na;
+                }
+            }
+#endif
+            if (nmv) sync_seq(q);
+            else wave_sync();
             CDCL_CLK(S, 2);
             if (conflict >= 0 || q.full) return conflict;
         }
@@ -533,7 +605,7 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef SATMI_CDCL_PHASES
     if (ln == 0) {
-        for (int i = 0; i < 7; ++i) S.clk[i] = 0;
+        for (int i = 0; i < 16; ++i) S.clk[i] = 0;
         S.clk[7] = __builtin_amdgcn_s_memtime();
     }
 #endif
@@ -657,6 +729,9 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
         st[7] = q.pool_top;
 #ifdef SATMI_CDCL_PHASES
         for (int i = 0; i < 4; ++i) st[4 + i] = (int64_t)S.clk[i];
+        for (int i = 0; i < 3; ++i) st[1 + i] = (int64_t)S.clk[4 + i];   // moves, entries, lists
+        // (over the model row) clocks in watch adds, in resizes, resizes, entries moved by them, adds
+        for (int i = 0; i < 5 && i < A.assign_stride; ++i) out[i] = (int32_t)min<uint64_t>(S.clk[8 + i], INT32_MAX);
 #endif
         A.var_inc[b] = q.var_inc;
     }
@@ -685,11 +760,8 @@ __global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
     S.wfill = (int32_t *)small(A.lay.wfill);
     S.wused = (int32_t *)small(A.lay.wused);
     S.pool = (int32_t *)(base + A.lay.pool);
-    S.snap = (int32_t *)(base + A.lay.snap);
-    S.rep = (int32_t *)(base + A.lay.rep);
-    S.slot = (int32_t *)(base + A.lay.slot);
 #ifdef SATMI_CDCL_PHASES
-    __shared__ uint64_t clk_s[8];
+    __shared__ uint64_t clk_s[16];
     S.clk = clk_s;
 #endif
     S.scratch = A.lay.lds_bytes ? (int32_t *)(cdcl_lds + A.lay.lds_scratch) : (int32_t *)(base + A.lay.scratch);
@@ -720,7 +792,6 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     // set tables: each clause sits in <= 2 sets; a table is < 8x its entries
     // over its lifetime (doubling tables, dummies until the next resize)
     const int64_t P = 16 * 2 * C + (int64_t)WS_MINSIZE * K;
-    const int64_t SN = 2 * C + 64;                           // largest snapshot
     auto a = [](uint64_t x) { return (x + 255u) & ~(uint64_t)255u; };
     uint64_t o = 0;
     L->coff = o;    o = a(o + 8 * (uint64_t)(C + 1));
@@ -738,9 +809,6 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     L->wfill = o;   o = a(o + 4 * (uint64_t)K);
     L->wused = o;   o = a(o + 4 * (uint64_t)K);
     L->pool = o;    o = a(o + 4 * (uint64_t)P);
-    L->snap = o;    o = a(o + 4 * (uint64_t)SN);
-    L->rep = o;     o = a(o + 4 * (uint64_t)SN);
-    L->slot = o;    o = a(o + 4 * (uint64_t)SN);
     L->lcap = (int32_t)std::min<int64_t>(2 * N + 2 + std::max(max_len, 1), INT32_MAX / 8);
     L->scratch = o; o = a(o + 4 * 2 * (uint64_t)L->lcap);   // two learned-literal lists
     L->bytes = o;
@@ -750,7 +818,6 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     L->clause_cap = C;
     L->lit_cap = Lc;
     L->pool_cap = P;
-    L->snap_cap = SN;
     L->ncap = max_vars;
     return max_vars >= 0 && max_vars < (1 << 29);
 }

@@ -1,0 +1,60 @@
+"""Where a CDCL iteration's time goes, on the bench's `cdcl` formulas.
+
+Diagnostic build only (never the product):
+    make -C sat-mpi-stana-andrei_amd variant VFLAGS=-DSATMI_CDCL_PHASES VNAME=libsatmi_cdclph.so
+    SATMI_LIB_VARIANT=libsatmi_cdclph.so python tools/cdcl_probe.py [--formulas N]
+
+The phase build overwrites the stats columns (csrc/cdcl.hip solve_one): [1..3]
+= watch moves, snapshot entries, false watch lists visited; [4..7] = shader
+clocks in snapshots, replacement watches, watch-list moves, and everything
+between propagate calls; the model row's first five entries = clocks in watch
+adds, clocks in table resizes, resizes, entries they moved, watch adds.  Printed per iteration over the iteration-capped
+solves (the launch's tail) and over the rest, plus the launch's wall time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sat-mpi-stana-andrei_amd"))
+
+from satmi import cnf  # noqa: E402
+from satmi.cdcl import CDCL_LIMIT, cdcl_batch_packed  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--formulas", type=int, default=32768)
+    ap.add_argument("--max-iter", type=int, default=10000)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--tag", default=os.environ.get("SATMI_LIB_VARIANT", "libsatmi.so"))
+    a = ap.parse_args()
+    hb = cnf.menu_batch(a.formulas, 80, 3, 15, seed=a.seed)
+    cdcl_batch_packed(hb, max_iter=a.max_iter, arrays=True)   # warm-up (arenas, code)
+    t = time.perf_counter()
+    r = cdcl_batch_packed(hb, max_iter=a.max_iter, arrays=True)
+    wall = time.perf_counter() - t
+    st, s = r["status"], r["stats"].astype(np.float64)
+    asg = r["assign"].astype(np.float64)   # (phase build: watch-add / resize clocks and counts)
+    out = {"lib": a.tag, "formulas": a.formulas, "wall_ms": wall * 1e3, "capped": int((st == CDCL_LIMIT).sum())}
+    for name, sel in (("capped", st == CDCL_LIMIT), ("rest", st != CDCL_LIMIT)):
+        it = s[sel, 0].sum()
+        if it == 0:
+            continue
+        out[name] = {"iterations": int(it),
+                     "per_iteration": {"moves": s[sel, 1].sum() / it, "snapshot_entries": s[sel, 2].sum() / it,
+                                       "false_lists": s[sel, 3].sum() / it,
+                                       "clk_snapshot": s[sel, 4].sum() / it, "clk_replacement": s[sel, 5].sum() / it,
+                                       "clk_moves": s[sel, 6].sum() / it, "clk_between": s[sel, 7].sum() / it,
+                                       "clk_watch_adds": asg[sel, 0].sum() / it, "clk_resizes": asg[sel, 1].sum() / it,
+                                       "resizes": asg[sel, 2].sum() / it, "resize_entries": asg[sel, 3].sum() / it,
+                                       "watch_adds": asg[sel, 4].sum() / it}}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
