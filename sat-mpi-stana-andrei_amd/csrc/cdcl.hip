@@ -14,13 +14,17 @@
 //     in stamp order (REF.py:258, :262);
 //   * activity / var_inc: IEEE double arithmetic in the reference's order
 //     (REF.py:355-357, :378), max() keeping the first maximal variable.
-// What runs across the wave's 64 lanes (everything else is lane 0):
+// What runs across the wave's 64 lanes (the rest runs on lane 0, every lane
+// keeping the same scalar state):
 //   * propagate (REF.py:269-304): the tables of all false watch literals are
 //     read as one stream in the reference's visiting order, one slot per lane;
 //     the replacement watch of every member (its first other literal that is
 //     free or true) is found in parallel; the first member without one is the
 //     conflict; the removals are dummy marks at known slots (no resize on
-//     discard), the adds go in order on lane 0 (they may create keys);
+//     discard), the adds go in order (they may create keys);
+//   * the set tables' adds: each linear-probe run read at once (one lane per
+//     slot) and settled by ballots; a resize clears the new table across the
+//     lanes and re-inserts against an occupancy bitmap in registers;
 //   * the all-assigned test (REF.py:257) over a bitmap of the variables that
 //     occur; select_variable's max over activities (REF.py:370-379);
 //     backtracking (REF.py:359-368); the model's dict order (a rank per stamp).
@@ -116,7 +120,8 @@ struct St {   // views into one wave's arena
 __device__ __forceinline__ int iabs(int x) { return x < 0 ? -x : x; }
 __device__ __forceinline__ int lcode(int lit) { return (iabs(lit) << 1) | (lit < 0 ? 1 : 0); }
 
-// Lane-0 state of the sequential parts, mirrored to every lane by broadcasts.
+// The solver's scalar state, kept identical on every lane (it changes only in
+// wave-uniform code).
 struct Seq {
     int64_t nf;        // formula length (clauses)
     int64_t nlits;     // literals stored
@@ -128,7 +133,12 @@ struct Seq {
     bool full;         // the arena ran out
 };
 
-__device__ bool ws_alloc(const CdclArgs &A, Seq &q, int64_t slots, int64_t *off) {
+// The set-table operations below are wave-uniform: every lane calls them with
+// the same arguments and keeps the same Seq (no broadcast needed afterwards);
+// the probes read a whole linear-probe run at once (one lane per slot), the
+// writes are made by lane 0, a resize clears and rebuilds the table across the
+// lanes.
+__device__ __forceinline__ bool ws_alloc(const CdclArgs &A, Seq &q, int64_t slots, int64_t *off) {
     if (q.pool_top + slots > A.lay.pool_cap) {
         q.full = true;
         return false;
@@ -138,6 +148,7 @@ __device__ bool ws_alloc(const CdclArgs &A, Seq &q, int64_t slots, int64_t *off)
     return true;
 }
 
+// set_insert_clean (lane 0; tables beyond the register bitmap of ws_resize)
 __device__ void ws_insert_clean(int32_t *t, uint64_t mask, int32_t key) {
     const uint64_t h = (uint64_t)(int64_t)(key - 1);
     uint64_t perturb = h, i = h & mask;
@@ -157,8 +168,14 @@ __device__ void ws_insert_clean(int32_t *t, uint64_t mask, int32_t key) {
     }
 }
 
-// set_table_resize(so, minused)  (lane 0)
+constexpr int64_t WS_BITMAP_SLOTS = 64 * 64;   // new tables up to this size: occupancy bits in registers
+
+// set_table_resize(so, minused) (wave-uniform): the new table cleared by all
+// lanes, the old members read 64 at a time and re-inserted in slot order
+// (set_insert_clean) against an occupancy bitmap held in registers (lane L:
+// slots [64L, 64L + 64)), so a probe costs no memory round trip
 __device__ void ws_resize(const CdclArgs &A, const St &S, Seq &q, int k, int64_t minused) {
+    const int ln = lane_id();
     int64_t newsize = WS_MINSIZE;
     while (newsize <= minused) newsize <<= 1;
     const int32_t mask = S.wmask[k];
@@ -167,122 +184,153 @@ __device__ void ws_resize(const CdclArgs &A, const St &S, Seq &q, int k, int64_t
     if (!ws_alloc(A, q, newsize, &off)) return;
 #ifdef SATMI_CDCL_PHASES
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    S.clk[10] += 1;
-    S.clk[11] += (uint64_t)S.wused[k];
+    if (ln == 0) {
+        S.clk[10] += 1;
+        S.clk[11] += (uint64_t)S.wused[k];
+    }
 #endif
-    int32_t *nt = S.pool + off, *ot = S.pool + S.woff[k];
-    for (int64_t i = 0; i < newsize; ++i) nt[i] = WS_EMPTY;
-    for (int64_t i = 0; i <= mask; ++i)
-        if (ot[i] != WS_EMPTY && ot[i] != WS_DUMMY) ws_insert_clean(nt, (uint64_t)(newsize - 1), ot[i]);
-    S.woff[k] = off;
-    S.wmask[k] = (int32_t)(newsize - 1);
-    S.wfill[k] = S.wused[k];
+    int32_t *nt = S.pool + off;
+    const int32_t *ot = S.pool + S.woff[k];
+    const uint64_t nmask = (uint64_t)(newsize - 1);
+    for (int64_t i = ln; i < newsize; i += 64) nt[i] = WS_EMPTY;
+    __builtin_amdgcn_s_waitcnt(0);   // the cleared slots land before the keys written over them
+    if (newsize <= WS_BITMAP_SLOTS) {
+        uint64_t occ = 0;   // this lane's 64 slots of the new table
+        for (int i0 = 0; i0 <= mask; i0 += 64) {
+            const int32_t x = i0 + ln <= mask ? ot[i0 + ln] : WS_EMPTY;
+            for (uint64_t am = __ballot(x != WS_EMPTY && x != WS_DUMMY); am; am &= am - 1) {
+                const int32_t key = __builtin_amdgcn_readlane(x, __builtin_ctzll(am));
+                const uint64_t h = (uint64_t)(int64_t)(key - 1);
+                uint64_t perturb = h, i = h & nmask, at;
+                for (;;) {
+                    // bits i .. i + WS_PROBES (a run never passes the table's end)
+                    const int w = (int)(i >> 6), sh = (int)(i & 63);
+                    const uint64_t lo = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)occ, w) |
+                                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(occ >> 32), w) << 32);
+                    uint64_t run = ~lo >> sh;   // free slots from i on
+                    if (sh > 0 && w + 1 < 64) {
+                        const uint64_t hi =
+                            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)occ, w + 1) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(occ >> 32), w + 1) << 32);
+                        run |= ~hi << (64 - sh);
+                    }
+                    const int len = i + WS_PROBES <= nmask ? WS_PROBES + 1 : 1;
+                    run &= (len == 64 ? ~0ull : (1ull << len) - 1);
+                    if (run) {
+                        at = i + (uint64_t)__builtin_ctzll(run);
+                        break;
+                    }
+                    perturb >>= WS_PERTURB;
+                    i = (i * 5 + 1 + perturb) & nmask;
+                }
+                if (ln == (int)(at >> 6)) occ |= 1ull << (at & 63);
+                if (ln == 0) nt[at] = key;
+            }
+        }
+    } else if (ln == 0) {
+        for (int64_t i = 0; i <= mask; ++i)
+            if (ot[i] != WS_EMPTY && ot[i] != WS_DUMMY) ws_insert_clean(nt, nmask, ot[i]);
+    }
+    if (ln == 0) {
+        S.woff[k] = off;
+        S.wmask[k] = (int32_t)nmask;
+        S.wfill[k] = S.wused[k];
+    }
+    wave_sync();
 #ifdef SATMI_CDCL_PHASES
-    S.clk[9] += __builtin_amdgcn_s_memtime() - t0;
+    if (ln == 0) S.clk[9] += __builtin_amdgcn_s_memtime() - t0;
 #endif
 }
 
-// set_add_entry(so, key, hash = key - 1)  (lane 0)
+// set_add_entry(so, key, hash = key - 1) (wave-uniform): each linear-probe run
+// (the slot and the WS_PROBES after it, when they fit) is read at once, one
+// lane per slot, and settled by ballots in probe order: the first empty slot
+// or the key itself ends the search; CPython 3.10 keeps the LAST dummy probed
+// before it as the slot to reuse
 __device__ void ws_add(const CdclArgs &A, const St &S, Seq &q, int k, int32_t key) {
+    const int ln = lane_id();
     const int64_t h = (int64_t)(key - 1);
     int32_t *t = S.pool + S.woff[k];
     const uint64_t mask = (uint64_t)S.wmask[k];
-    uint64_t i = (uint64_t)h & mask;
-    int64_t slot = (int64_t)i;
-    if (t[i] != WS_EMPTY) {
-        int64_t freeslot = -1;
-        uint64_t perturb = (uint64_t)h;
-        for (;;) {
-            int32_t x = t[i];
-            if (x == key) return;
-            if (x == WS_DUMMY) freeslot = (int64_t)i;   // CPython 3.10 keeps the LAST dummy probed
-            bool hit_empty = false;
-            if (i + WS_PROBES <= mask) {
-                for (int j = 1; j <= WS_PROBES; ++j) {
-                    x = t[i + j];
-                    if (x == WS_EMPTY) {
-                        slot = (int64_t)(i + j);
-                        hit_empty = true;
-                        break;
-                    }
-                    if (x == key) return;
-                    if (x == WS_DUMMY) freeslot = (int64_t)(i + j);
-                }
-            }
-            if (!hit_empty) {
-                perturb >>= WS_PERTURB;
-                i = (i * 5 + 1 + perturb) & mask;
-                if (t[i] != WS_EMPTY) continue;
-                slot = (int64_t)i;
-            }
-            if (freeslot >= 0) {   // found_unused_or_dummy with a dummy on the way
-                S.wused[k]++;
-                t[freeslot] = key;
-                return;
-            }
+    uint64_t i = (uint64_t)h & mask, perturb = (uint64_t)h;
+    int64_t freeslot = -1, slot;
+    for (;;) {
+        const int probes = i + WS_PROBES <= mask ? WS_PROBES : 0;
+        const bool in = ln <= probes;
+        const int32_t x = in ? t[i + ln] : 0;
+        const uint64_t em = __ballot(in && x == WS_EMPTY), km = __ballot(in && x == key),
+                       dm = __ballot(in && x == WS_DUMMY);
+        const uint64_t stop = em | km;
+        const uint64_t before = stop ? (1ull << __builtin_ctzll(stop)) - 1 : ~0ull;
+        if (dm & before) freeslot = (int64_t)(i + 63 - __builtin_clzll(dm & before));
+        if (stop) {
+            if (km & (stop & (0 - stop))) return;   // already a member
+            slot = (int64_t)(i + __builtin_ctzll(stop));
             break;
         }
+        perturb >>= WS_PERTURB;
+        i = (i * 5 + 1 + perturb) & mask;
     }
-    S.wfill[k]++;
-    S.wused[k]++;
-    t[slot] = key;
-    if ((uint64_t)S.wfill[k] * 5 < mask * 3) return;
-    const int64_t used = S.wused[k];
-    ws_resize(A, S, q, k, used > 50000 ? used * 2 : used * 4);
+    if (freeslot >= 0) {   // found_unused_or_dummy with a dummy on the way
+        if (ln == 0) {
+            S.wused[k]++;
+            t[freeslot] = key;
+        }
+        wave_sync();
+        return;
+    }
+    const int32_t fill = S.wfill[k] + 1, used = S.wused[k] + 1;
+    if (ln == 0) {
+        S.wfill[k] = fill;
+        S.wused[k] = used;
+        t[slot] = key;
+    }
+    wave_sync();
+    if ((uint64_t)fill * 5 < mask * 3) return;
+    ws_resize(A, S, q, k, used > 50000 ? (int64_t)used * 2 : (int64_t)used * 4);
 }
 
-// self.watch_list[lit] (defaultdict: a missing key is created with an empty set)  (lane 0)
+// self.watch_list[lit] (defaultdict: a missing key is created with an empty set)
 __device__ int key_of(const CdclArgs &A, const St &S, Seq &q, int lit) {
+    const int ln = lane_id();
     const int c = lcode(lit);
     int k = S.kidx[c] - 1;
     if (k >= 0) return k;
     int64_t off;
     if (!ws_alloc(A, q, WS_MINSIZE, &off)) return -1;
     k = q.nk++;
-    S.klit[k] = lit;
-    S.kidx[c] = k + 1;
-    S.woff[k] = off;
-    S.wmask[k] = WS_MINSIZE - 1;
-    S.wfill[k] = S.wused[k] = 0;
-    for (int i = 0; i < WS_MINSIZE; ++i) S.pool[off + i] = WS_EMPTY;
+    if (ln == 0) {
+        S.klit[k] = lit;
+        S.kidx[c] = k + 1;
+        S.woff[k] = off;
+        S.wmask[k] = WS_MINSIZE - 1;
+        S.wfill[k] = S.wused[k] = 0;
+    }
+    if (ln < WS_MINSIZE) S.pool[off + ln] = WS_EMPTY;
+    wave_sync();
     return k;
 }
 
+// self.watch_list[lit].add(idx) (wave-uniform)
 __device__ void watch_add(const CdclArgs &A, const St &S, Seq &q, int lit, int64_t idx) {
 #ifdef SATMI_CDCL_PHASES
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
+    lit = __builtin_amdgcn_readfirstlane(lit);
+    const int32_t key = __builtin_amdgcn_readfirstlane((int32_t)(idx + 1));
     const int k = key_of(A, S, q, lit);
-    if (k >= 0 && !q.full) ws_add(A, S, q, k, (int32_t)(idx + 1));
+    if (k >= 0 && !q.full) ws_add(A, S, q, k, key);
 #ifdef SATMI_CDCL_PHASES
-    S.clk[8] += __builtin_amdgcn_s_memtime() - t0;   // (lane 0)
-    S.clk[12] += 1;
+    if (lane_id() == 0) {
+        S.clk[8] += __builtin_amdgcn_s_memtime() - t0;
+        S.clk[12] += 1;
+    }
 #endif
 }
 
 __device__ __forceinline__ bool lit_false(const St &S, int lit) {
     const int8_t v = S.val[iabs(lit)];
     return v >= 0 && (lit > 0) != (v != 0);
-}
-
-// Broadcast lane 0's Seq to the wave (after lane-0 sections).
-__device__ void sync_seq(Seq &q) {
-    wave_sync();
-    q.nf = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q.nf) |
-           ((int64_t)__builtin_amdgcn_readfirstlane((int)(q.nf >> 32)) << 32);
-    q.nlits = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q.nlits) |
-              ((int64_t)__builtin_amdgcn_readfirstlane((int)(q.nlits >> 32)) << 32);
-    q.pool_top = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q.pool_top) |
-                 ((int64_t)__builtin_amdgcn_readfirstlane((int)(q.pool_top >> 32)) << 32);
-    q.next_ord = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q.next_ord) |
-                 ((int64_t)__builtin_amdgcn_readfirstlane((int)(q.next_ord >> 32)) << 32);
-    q.nk = __builtin_amdgcn_readfirstlane(q.nk);
-    q.level = __builtin_amdgcn_readfirstlane(q.level);
-    const uint64_t vb = __double_as_longlong(q.var_inc);
-    q.var_inc = __longlong_as_double((long long)((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)vb) |
-                                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(vb >> 32))
-                                                  << 32)));
-    q.full = __builtin_amdgcn_readfirstlane((int)q.full) != 0;
 }
 
 // propagate (REF.py:269-304): returns the conflict clause's index, -1 for none.
@@ -299,7 +347,7 @@ __device__ void sync_seq(Seq &q) {
 // member of a window looks for its replacement watch at the same time; the
 // first member without one (stream order) is the conflict (REF.py:292-293),
 // and the members before it move: dummies at their slots, the adds in stream
-// order on lane 0 (they may create keys and resize tables).  A launch's long
+// order (they may create keys and resize tables).  A launch's long
 // solves are latency-bound chains of dependent memory reads, and one window
 // covers the false lists of a typical pass at once.
 constexpr int CDCL_LITS_AHEAD = 4;   // a member's first literals read at once
@@ -403,22 +451,24 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             CDCL_CLK(S, 1);
             // the moves: self.watch_list[lit].remove(idx) (a dummy at its slot),
             // self.watch_list[other_lit].add(idx) in stream order
+#ifdef SATMI_CDCL_PHASES
             int nmv = 0;
+#endif
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const bool mv = act[u] && r[u] != 0 && (u < cu || (u == cu && ln < cl));
                 if (mv) S.pool[at[u]] = WS_DUMMY;
                 uint64_t mm = __ballot(mv);
+#ifdef SATMI_CDCL_PHASES
                 nmv += __popcll(mm);
+#endif
                 for (; mm; mm &= mm - 1) {
                     const int l = __builtin_ctzll(mm);
                     const int rl = __builtin_amdgcn_readlane(r[u], l);
                     const int cx = __builtin_amdgcn_readlane(x[u], l);
                     const int kl = k0 + __builtin_amdgcn_readlane(own[u], l);
-                    if (ln == 0) {
-                        S.wused[kl] -= 1;
-                        if (!q.full) watch_add(A, S, q, rl, (int64_t)cx - 1);
-                    }
+                    if (ln == 0) S.wused[kl] -= 1;
+                    if (!q.full) watch_add(A, S, q, rl, (int64_t)cx - 1);
                 }
             }
 #ifdef SATMI_CDCL_PHASES
@@ -432,8 +482,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                 }
             }
 #endif
-            if (nmv) sync_seq(q);
-            else wave_sync();
+            wave_sync();
             CDCL_CLK(S, 2);
             if (conflict >= 0 || q.full) return conflict;
         }
@@ -583,25 +632,26 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
     q.level = 0;
     q.var_inc = 1.0;
     q.full = false;
-    // setup_watch_list (REF.py:233-244)
-    if (ln == 0) {
-        for (int64_t i = 0; i < m && !q.full; ++i) {
-            const int64_t jb = S.coff[i], len = S.coff[i + 1] - jb;
-            if (len > 1) {
-                watch_add(A, S, q, S.lits[jb], i);
-                watch_add(A, S, q, S.lits[jb + 1], i);
-            } else if (len == 1) {
-                const int x = S.lits[jb], v = iabs(x);
-                if (S.val[v] < 0) {
+    // setup_watch_list (REF.py:233-244), wave-uniform
+    for (int64_t i = 0; i < m && !q.full; ++i) {
+        const int64_t jb = S.coff[i], len = S.coff[i + 1] - jb;
+        if (len > 1) {
+            watch_add(A, S, q, S.lits[jb], i);
+            watch_add(A, S, q, S.lits[jb + 1], i);
+        } else if (len == 1) {
+            const int x = S.lits[jb], v = iabs(x);
+            if (S.val[v] < 0) {
+                if (ln == 0) {
                     S.val[v] = x > 0;
-                    S.ord[v] = q.next_ord++;
+                    S.ord[v] = q.next_ord;
                     S.lev[v] = 0;
                     S.ante[v] = i;
                 }
+                ++q.next_ord;
             }
+            wave_sync();
         }
     }
-    sync_seq(q);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef SATMI_CDCL_PHASES
     if (ln == 0) {
@@ -624,28 +674,28 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
             ++conflicts;
             int32_t bt = 0;
             int32_t cnt = analyze_conflict(S, conflict, A.lay.lcap, &bt);   // the whole wave
-            if (ln == 0) {
-                if (cnt > 0) {   // learn_clause (REF.py:347-357)
-                    if (q.nf + 1 > A.lay.clause_cap || q.nlits + cnt > A.lay.lit_cap) {
-                        q.full = true;
-                    } else {
-                        const int64_t idx = q.nf;
-                        for (int i = 0; i < cnt; ++i) S.lits[q.nlits + i] = S.scratch[i];
-                        q.nlits += cnt;
-                        S.coff[idx + 1] = q.nlits;
-                        q.nf = idx + 1;
-                        if (cnt > 1) {
-                            watch_add(A, S, q, S.scratch[0], idx);
-                            watch_add(A, S, q, S.scratch[1], idx);
-                        }
-                        q.var_inc *= 1.0 / VAR_DECAY;
-                        for (int i = 0; i < cnt; ++i) S.act[iabs(S.scratch[i])] += q.var_inc;
-                    }
-                }
-            }
-            sync_seq(q);
             cnt = __builtin_amdgcn_readfirstlane(cnt);
             bt = __builtin_amdgcn_readfirstlane(bt);
+            if (cnt > 0) {   // learn_clause (REF.py:347-357), wave-uniform
+                if (q.nf + 1 > A.lay.clause_cap || q.nlits + cnt > A.lay.lit_cap) {
+                    q.full = true;
+                } else {
+                    const int64_t idx = q.nf;
+                    for (int i = ln; i < cnt; i += 64) S.lits[q.nlits + i] = S.scratch[i];
+                    q.nlits += cnt;
+                    if (ln == 0) S.coff[idx + 1] = q.nlits;
+                    q.nf = idx + 1;
+                    if (cnt > 1) {
+                        watch_add(A, S, q, S.scratch[0], idx);
+                        watch_add(A, S, q, S.scratch[1], idx);
+                    }
+                    q.var_inc *= 1.0 / VAR_DECAY;
+                    // (in order on one lane: a variable can repeat in the list)
+                    if (ln == 0)
+                        for (int i = 0; i < cnt; ++i) S.act[iabs(S.scratch[i])] += q.var_inc;
+                    wave_sync();
+                }
+            }
             if (cnt == -2) q.full = true;   // scratch list bound (see analyze_conflict)
             else if (cnt < 0) {
                 status = CD_ERROR;
@@ -697,11 +747,12 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
             ++decisions;
             if (ln == 0) {
                 S.val[bv] = 1;
-                S.ord[bv] = q.next_ord++;
+                S.ord[bv] = q.next_ord;
                 S.lev[bv] = q.level;
                 S.ante[bv] = ANTE_ABSENT;
             }
-            sync_seq(q);
+            ++q.next_ord;
+            wave_sync();
         }
     }
     if (q.full) status = CD_FULL;

@@ -142,3 +142,26 @@ def test_cdcl_arena_form_beyond_lds():
         _check(r, o["result"], o["assignment"], o["var_inc"],
                {k: o["stats"][k] for k in ("iterations", "conflicts", "decisions", "learned", "clauses",
                                            "watch_keys", "level")})
+
+
+def test_cdcl_large_watch_tables():
+    """Thousands of clauses watched by the same few literals: set tables grow
+    past the register occupancy bitmap of a resize (csrc/cdcl.hip
+    WS_BITMAP_SLOTS = 4,096 slots: beyond it the re-insertion probes memory),
+    collide along linear-probe runs and perturbation, and fill with dummies as
+    the watches move; against the oracle."""
+    rng = random.Random(23)
+    fs = []
+    for n, m in ((10, 1500), (12, 2600), (8, 900), (14, 3200)):
+        f = []
+        for _ in range(m):
+            first = rng.choice((1, -1, 2))   # few watch lists take most clauses
+            rest = [v if rng.random() < 0.5 else -v for v in rng.sample(range(3, n + 1), rng.randint(1, 3))]
+            f.append([first] + rest)
+        fs.append(f)
+    rs = cdcl_batch(fs, max_iter=300)
+    for f, r in zip(fs, rs):
+        o = oracle.cdcl(f, 300)
+        _check(r, o["result"], o["assignment"], o["var_inc"],
+               {k: o["stats"][k] for k in ("iterations", "conflicts", "decisions", "learned", "clauses",
+                                           "watch_keys", "level")})
