@@ -690,9 +690,26 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
                         watch_add(A, S, q, S.scratch[1], idx);
                     }
                     q.var_inc *= 1.0 / VAR_DECAY;
-                    // (in order on one lane: a variable can repeat in the list)
-                    if (ln == 0)
+                    if (cnt <= 64) {
+                        // a variable's increments in list order by the lane of its
+                        // first occurrence (a repeated variable adds var_inc once
+                        // per occurrence, REF.py:356-357)
+                        const int v = ln < cnt ? iabs(S.scratch[ln]) : -1;
+                        bool dup = false;
+                        int mult = 0;
+                        for (int j = 0; j < cnt; ++j) {
+                            const int vj = __builtin_amdgcn_readlane(v, j);
+                            dup |= j < ln && vj == v;
+                            mult += vj == v ? 1 : 0;
+                        }
+                        if (ln < cnt && !dup) {
+                            double a = S.act[v];
+                            for (int t = 0; t < mult; ++t) a += q.var_inc;
+                            S.act[v] = a;
+                        }
+                    } else if (ln == 0) {
                         for (int i = 0; i < cnt; ++i) S.act[iabs(S.scratch[i])] += q.var_inc;
+                    }
                     wave_sync();
                 }
             }
@@ -722,22 +739,25 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
             }
             // select_variable (REF.py:370-379): the first unassigned variable of
             // maximal activity among 1..max(abs(l)); n is that maximum
-            double best = -1.0;
+            // (activities are sums of positive increments: >= 0, possibly
+            // +inf, never NaN, so their IEEE bit patterns order as unsigned
+            // integers; three DPP reductions: high word, low word, first variable)
+            uint64_t best = 0;
             int bv = INT_MAX;
             for (int v = 1 + ln; v <= n; v += 64)
-                if (S.val[v] < 0 && (bv == INT_MAX || S.act[v] > best)) {
-                    best = S.act[v];
-                    bv = v;
+                if (S.val[v] < 0) {
+                    const uint64_t a = (uint64_t)__double_as_longlong(S.act[v]);
+                    if (bv == INT_MAX || a > best) {
+                        best = a;
+                        bv = v;
+                    }
                 }
-            for (int off = 32; off >= 1; off >>= 1) {
-                const double ob = __shfl_xor(best, off, 64);
-                const int ov = __shfl_xor(bv, off, 64);
-                if (ov != INT_MAX && (bv == INT_MAX || ob > best || (ob == best && ov < bv))) {
-                    best = ob;
-                    bv = ov;
-                }
-            }
-            bv = __builtin_amdgcn_readfirstlane(bv);
+            const bool has = bv != INT_MAX;
+            const uint32_t bh = (uint32_t)(best >> 32), bl = (uint32_t)best;
+            const uint32_t mh = wave_max_u32(has ? bh : 0u);
+            const bool on_h = has && bh == mh;
+            const uint32_t ml = wave_max_u32(on_h ? bl : 0u);
+            bv = wave_min_i32(on_h && bl == ml ? bv : INT_MAX);
             if (bv == INT_MAX) {   // no unassigned variable: True (REF.py:261-262)
                 status = CD_TRUE;
                 break;
