@@ -304,8 +304,10 @@ struct ResState {
     unsigned long long count;     // claims of the last pass
     int64_t passes;
     int64_t pairs, candidates;    // whole saturation
+    int64_t stripe_max;           // the last pass's largest stripe count (sizes a regrown stage)
     uint64_t t0;                  // s_memrealtime at the start
-    int32_t done, result, empty, timeout, overflow, pad;
+    int32_t done, result, empty, timeout, overflow;
+    int32_t spill;                // the pass's new keys outgrew the stage: counted, not stored
 };
 
 struct ResArgs {
@@ -334,6 +336,18 @@ constexpr int RES_STRIPES = 64;
 // runs again on a larger table -- instead of probing a full table for ever.
 constexpr int RES_PROBE_MAX = 32;
 constexpr int RES_BUCKET = 8;             // slots per bucket: one 64-B read checks them all
+
+// a saturation's starting state and append stripes (one block of 2 x RES_STRIPES threads)
+__global__ void res_init_kernel(ResState *S, int64_t ncl, unsigned long long *stripes, int64_t slot_base) {
+    const int t = threadIdx.x;
+    if (t < 2 * RES_STRIPES) stripes[t] = t < RES_STRIPES ? (unsigned long long)slot_base : 0ull;
+    if (t == 0) {
+        ResState z{};
+        z.ncl = ncl;
+        z.result = -1;
+        *S = z;
+    }
+}
 
 __global__ void __launch_bounds__(256) res_pack_kernel(const uint64_t *k2, int64_t n, uint64_t *keys, ResState *S) {
     if (blockIdx.x == 0 && threadIdx.x == 0) S->t0 = __builtin_amdgcn_s_memrealtime();
@@ -407,8 +421,9 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
     // tiles ~ (ncl - jlo) / tj x ncl / 512 (the triangle) ~ RES_TILES
     const int tj = (int)max<int64_t>(1, min<int64_t>(RES_TJ, (ncl - jlo) * (ncl / 512 + 1) / RES_TILES));
     int cand = 0;
+    bool halt = false;   // block-uniform: a flag or the deadline ended the pass
     const int64_t njt = (ncl - jlo + tj - 1) / tj;
-    for (int64_t jt = blockIdx.x; jt < njt; jt += gridDim.x) {
+    for (int64_t jt = blockIdx.x; jt < njt && !halt; jt += gridDim.x) {
         const int64_t j0 = jlo + jt * tj, j1 = min<int64_t>(j0 + tj, ncl);
         const int nj = (int)(j1 - j0);
         for (int64_t i0 = (int64_t)blockIdx.y * 256; i0 < j1 - 1; i0 += (int64_t)gridDim.y * 256) {
@@ -424,12 +439,20 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
             }
             if (tid < nj) jk[tid] = A.keys[j0 + tid];
             __syncthreads();
-            if (sh_stop) break;   // block-uniform
+            if (sh_stop) {   // block-uniform
+                halt = true;
+                break;
+            }
             const int64_t i = i0 + tid;
             const uint64_t a = i < j1 ? A.keys[i] : 0ull;
             const uint32_t Pa = (uint32_t)a, Na = (uint32_t)(a >> 32);
             const int first = (int)max<int64_t>(0, i + 1 - j0);   // j's of this tile above i
             for (int jj = 0; jj < nj; ++jj) {
+                // the deadline inside the tile too (per wave, every 8 clauses j)
+                if ((jj & 7) == 7 && A.limit_ticks && __builtin_amdgcn_s_memrealtime() - t0 > A.limit_ticks) {
+                    if (ln == 0) __hip_atomic_store(&S->timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
                 bool win = false;
                 uint64_t r = 0;
                 if (jj >= first && i < j1) {
@@ -466,8 +489,8 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
                                 (int64_t)(atomicAdd(A.stripes + stripe, 1ull) - (unsigned long long)A.slot_base);
                             if (idx < A.stage_region)
                                 A.stage[stripe * A.stage_region + idx] = r;
-                            else
-                                __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            else   // counted, not stored: the pass goes on, so its count is exact
+                                __hip_atomic_store(&S->spill, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         }
                     }
                 }
@@ -482,7 +505,7 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
                     if (f0 + t < A.stage_region)
                         A.stage[stripe * A.stage_region + f0 + t] = abuf[t];
                     else
-                        __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&S->spill, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             __syncthreads();   // jk / abuf / sh_stop are rewritten by the next tile
@@ -504,6 +527,11 @@ __global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
     __shared__ int64_t pre[RES_STRIPES + 1];
     ResState *S = A.st;
     if (S->done || S->overflow) return;
+    if (S->spill) {   // the stage held a part of the pass's keys: the host regrows it and runs the pass again
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+            __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (threadIdx.x == 0) {
         int64_t acc = 0;
         for (int t = 0; t < RES_STRIPES; ++t) {
@@ -565,12 +593,14 @@ __global__ void __launch_bounds__(RES_STRIPES) res_finish_pass_kernel(ResArgs A)
     A.stripes[RES_STRIPES + t] = 0ull;
     __syncthreads();
     if (t != 0) return;
-    int64_t claims = 0, cands = 0;
+    int64_t claims = 0, cands = 0, smax = 0;
     for (int k = 0; k < RES_STRIPES; ++k) {
         claims += cnt[k];
         cands += cand[k];
+        smax = max(smax, cnt[k]);
     }
     if (S->done) return;
+    S->stripe_max = smax;
     S->count = (unsigned long long)claims;   // this pass's claims (a regrowth is sized by them)
     S->candidates += cands;
     finish_pass(A, S, claims);
@@ -606,6 +636,27 @@ struct DevBuf {
     }
     template <class T>
     T *as() const { return (T *)p; }
+};
+
+// Pinned host memory, grow-only: the call's inputs are gathered here and sent
+// in one copy (a copy from pageable memory is staged synchronously, one per
+// array), and small results come back through it.
+struct PinBuf {
+    unsigned char *p = nullptr;
+    size_t cap = 0;
+    ~PinBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    int reserve(size_t bytes) {
+        if (bytes <= cap) return SATMI_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max(bytes, (size_t)4096);
+        SATMI_HIP(hipHostMalloc((void **)&p, want, hipHostMallocDefault));
+        cap = want;
+        return SATMI_OK;
+    }
 };
 
 #define SATMI_TRY(x)                  \
@@ -678,8 +729,10 @@ struct EventTimer {
 // calls.  A saturation of a small formula is a few passes of small launches,
 // so allocating its buffers per call cost more than its kernels.
 struct ResWork {
-    DevBuf d_off, d_lits, d_map, clauses, cand, counters, table, flag, pos, slotv, tiles, grand;
+    DevBuf clauses, cand, counters, table, flag, pos, slotv, tiles, grand;
     DevBuf keys, state, passnew, stage, stripes;   // the packed path
+    DevBuf up;                                     // the call's inputs (one copy from up_h)
+    PinBuf up_h, down_h;                           // pinned staging: inputs, per-pass counts
     EventTimer t_pairs, t_claims;
     hipStream_t stream = nullptr;
     unsigned long long *pin = nullptr;   // pinned host words: the per-chunk counters and claim count
@@ -797,6 +850,7 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
                       int64_t rec_lit_cap, int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_pass_off,
                       int rec_pass_cap) {
     hipStream_t s = wk.stream;
+    const auto t_call = std::chrono::steady_clock::now();
     const int PCAP = 1 << 12;   // passes whose counts the device keeps (the host copies out pass_cap of them)
     SATMI_TRY(wk.keys.reserve(8 * (size_t)std::max<int64_t>(4 * (int64_t)nclauses, 1 << 14)));
     SATMI_TRY(wk.state.reserve(sizeof(ResState)));
@@ -805,9 +859,6 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     int64_t key_cap = (int64_t)(wk.keys.cap / 8);
     // stripe regions: twice the key room (the stripes fill unevenly)
     SATMI_TRY(wk.stage.reserve(8 * 2 * (size_t)key_cap));
-    std::vector<unsigned long long> stripes0(2 * RES_STRIPES, 0ull);
-    for (int t = 0; t < RES_STRIPES; ++t) stripes0[t] = (unsigned long long)slot_base;
-    SATMI_HIP(hipMemcpyAsync(wk.stripes.p, stripes0.data(), 8 * 2 * RES_STRIPES, hipMemcpyHostToDevice, s));
     // the table: a power of two >= 2x the keys it can hold (load <= 1/2; a
     // table larger than needed only spreads the probes over more cache lines)
     const auto slots_for = [](int64_t nkeys) {   // a power of two, >= 8 buckets
@@ -817,22 +868,18 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     };
     uint64_t tslots = slots_for(key_cap);
     SATMI_TRY(wk.table.reserve(8 * tslots));
+    // the state and the stripes set on the device (no copies from the host),
+    // then the keys packed; the deadline is measured from the pack kernel's
+    // start (t0 written by it; no clauses: no pairs, the deadline is never read)
+    hipLaunchKernelGGL(res_init_kernel, dim3(1), dim3(2 * RES_STRIPES), 0, s, wk.state.as<ResState>(),
+                       (int64_t)nclauses, wk.stripes.as<unsigned long long>(), slot_base);
     if (nclauses > 0)
         hipLaunchKernelGGL(res_pack_kernel, dim3(grid_for(nclauses)), dim3(256), 0, s, wk.clauses.as<uint64_t>(),
                            (int64_t)nclauses, wk.keys.as<uint64_t>(), wk.state.as<ResState>());
-    ResState &st = *wk.pst;
+    ResState &st = *wk.pst;   // the host's copy, refreshed after each batch of passes
     st = ResState{};
     st.ncl = nclauses;
     st.result = -1;
-    // the deadline is measured on the device from the pack kernel's start (t0
-    // written by it): copy the state behind it without t0
-    const auto push_state = [&]() -> int {
-        SATMI_HIP(hipMemcpyAsync(wk.state.p, wk.pst, offsetof(ResState, t0), hipMemcpyHostToDevice, s));
-        SATMI_HIP(hipMemcpyAsync((char *)wk.state.p + offsetof(ResState, done), &wk.pst->done,
-                                 sizeof(ResState) - offsetof(ResState, done), hipMemcpyHostToDevice, s));
-        return SATMI_OK;
-    };
-    SATMI_TRY(push_state());   // (no clauses: no pairs, the deadline is never read)
     const auto seed = [&](int64_t nkeys) -> int {   // a fresh table holding keys [0, nkeys)
         SATMI_HIP(hipMemsetAsync(wk.table.p, 0xFF, 8 * tslots, s));   // HT_EMPTY
         if (nkeys > 0)
@@ -886,17 +933,26 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         SATMI_HIP(hipMemcpyAsync(wk.pst, wk.state.p, sizeof(ResState), hipMemcpyDeviceToHost, s));
         SATMI_HIP(hipStreamSynchronize(s));
         if (st.overflow) {   // grow the key buffer and / or the table, re-seed, run the pass again
+            if (time_limit_s > 0 &&
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t_call).count() >= time_limit_s)
+                break;   // past the deadline: a timeout after the completed passes (result -1)
             // twice the claims of the stopped pass (all of its new keys when
-            // only the key buffer ran out; a part of them when it stopped early)
+            // the pass ran to its end -- the key buffer or the stage ran out,
+            // the stage's excess counted, not stored; a part of them when the
+            // table stopped it early)
             const int64_t claims = (int64_t)st.count;
             const int64_t want = std::max<int64_t>(2 * key_cap, st.ncl + 2 * claims + 1024);
             SATMI_TRY(grow_keys(wk, want, st.ncl, s));
             key_cap = (int64_t)(wk.keys.cap / 8);
-            SATMI_TRY(wk.stage.reserve(8 * 2 * (size_t)key_cap));   // (the finish kernel reset the stripes)
+            // stripe regions: twice the key room, and 5/4 of the fullest stripe
+            // of the stopped pass (the finish kernel reset the stripes)
+            const int64_t region = std::max<int64_t>(2 * key_cap / RES_STRIPES, st.stripe_max + st.stripe_max / 4 + 1024);
+            SATMI_TRY(wk.stage.reserve(8 * (size_t)RES_STRIPES * (size_t)region));
             tslots = slots_for(key_cap);
             SATMI_TRY(wk.table.reserve(8 * tslots));
             args();
             st.overflow = 0;
+            st.spill = 0;
             st.done = 0;
             st.empty = 0;
             st.timeout = 0;
@@ -917,9 +973,12 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         if (st.done) break;
     }
     const int np = (int)std::min<int64_t>(st.passes, std::min(pass_cap, PCAP));
-    if (h_pass_new && np > 0)
-        SATMI_HIP(hipMemcpyAsync(h_pass_new, wk.passnew.p, 8 * (size_t)np, hipMemcpyDeviceToHost, s));
+    if (h_pass_new && np > 0) {   // through pinned memory (a copy into pageable memory is staged)
+        SATMI_TRY(wk.down_h.reserve(8 * (size_t)np));
+        SATMI_HIP(hipMemcpyAsync(wk.down_h.p, wk.passnew.p, 8 * (size_t)np, hipMemcpyDeviceToHost, s));
+    }
     SATMI_HIP(hipStreamSynchronize(s));
+    if (h_pass_new && np > 0) std::memcpy(h_pass_new, wk.down_h.p, 8 * (size_t)np);
     *h_result = st.result;
     *h_passes = (int32_t)st.passes;
     g_stats.pairs = st.pairs;
@@ -1010,20 +1069,26 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
     }
     ResWork *wk = lease.w;
     hipStream_t s = wk->stream;
-    DevBuf &d_off = wk->d_off, &d_lits = wk->d_lits, &d_map = wk->d_map, &clauses = wk->clauses, &cand = wk->cand,
-           &counters = wk->counters;
-    SATMI_TRY(d_off.reserve(4 * (size_t)(nclauses + 1)));
-    SATMI_TRY(d_lits.reserve(4 * (size_t)std::max<int64_t>(L, 1)));
-    SATMI_TRY(d_map.reserve(4 * (size_t)(maxvar + 1)));
+    DevBuf &clauses = wk->clauses, &cand = wk->cand, &counters = wk->counters;
+    // the clause offsets, the literals and the variable map in one pinned
+    // staging buffer, sent in one copy
+    const auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_lits = al(4 * (size_t)(nclauses + 1)), o_map = o_lits + al(4 * (size_t)std::max<int64_t>(L, 1));
+    const size_t up_bytes = o_map + al(4 * (size_t)(maxvar + 1));
+    SATMI_TRY(wk->up.reserve(up_bytes));
+    SATMI_TRY(wk->up_h.reserve(up_bytes));
     int64_t ncl = nclauses;
     SATMI_TRY(clauses.reserve(8 * (size_t)std::max<int64_t>(ncl, 1) * K));
     SATMI_TRY(counters.reserve(64));
     if (nclauses > 0) {
-        SATMI_HIP(hipMemcpyAsync(d_off.p, h_clause_off, 4 * (size_t)(nclauses + 1), hipMemcpyHostToDevice, s));
-        if (L) SATMI_HIP(hipMemcpyAsync(d_lits.p, h_lits, 4 * (size_t)L, hipMemcpyHostToDevice, s));
-        SATMI_HIP(hipMemcpyAsync(d_map.p, var2dense.data(), 4 * (size_t)(maxvar + 1), hipMemcpyHostToDevice, s));
+        // (the previous call's copy out of up_h finished: every call ends with a wait)
+        std::memcpy(wk->up_h.p, h_clause_off, 4 * (size_t)(nclauses + 1));
+        if (L) std::memcpy(wk->up_h.p + o_lits, h_lits, 4 * (size_t)L);
+        std::memcpy(wk->up_h.p + o_map, var2dense.data(), 4 * (size_t)(maxvar + 1));
+        SATMI_HIP(hipMemcpyAsync(wk->up.p, wk->up_h.p, up_bytes, hipMemcpyHostToDevice, s));
+        const unsigned char *up = (const unsigned char *)wk->up.p;
         hipLaunchKernelGGL(encode_keys_kernel, dim3(grid_for(nclauses)), dim3(PRIM_BLOCK), 0, s, nclauses,
-                           d_off.as<int32_t>(), d_lits.as<int32_t>(), d_map.as<int32_t>(), W,
+                           (const int32_t *)up, (const int32_t *)(up + o_lits), (const int32_t *)(up + o_map), W,
                            clauses.as<uint64_t>());
         SATMI_HIP(hipGetLastError());
     }
