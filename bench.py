@@ -752,7 +752,7 @@ def legs_main(args):
         keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_issue",
                 "cpu_baseline", "result", "passes_or_steps", "instances_per_s", "unit_props_per_s",
                 "capped_fraction", "sat_fraction", "sat", "unsat", "iteration_capped", "iterations_per_s",
-                "verdict_sha", "kernel_ms", "wave_utilisation")
+                "verdict_sha", "kernel_ms", "wave_utilisation", "oracle_check")
         out[name] = {k: r[k] for k in keep if k in r}
         out[name]["leg_wall_s"] = time.perf_counter() - t
     print(json.dumps(out), flush=True)
@@ -780,8 +780,11 @@ def main():
         out["configs"] = json.loads(r.stdout.strip().splitlines()[-1])
         out["configs_note"] = ("the other BASELINE configs, measured after the headline by a child process "
                                "(bench.py --legs-only, GPU_MAX_HW_QUEUES=17) with the same harness; "
-                               "configs[1] reported on 2 streams (one batch of 4,096 in flight behind another) "
-                               "and on 16 streams (16 resident batches, ~65 k instances in flight)")
+                               "configs[1] ('4,096 instances, n=50, on 1 MI355X') is answered by the 2-stream "
+                               "leg: batches of 4,096 solved back to back, the next batch's waves taking the CUs "
+                               "the current batch's tail leaves idle (at most 8,192 instances resident); the "
+                               "16-stream leg (16 batches resident, ~65 k instances in flight) is a saturation "
+                               "ceiling for a stream of such batches, not the configs[1] figure")
     if rank == 0:
         out["wall_s"] = time.perf_counter() - t_start
         print(json.dumps(out), flush=True)
