@@ -1,29 +1,43 @@
-"""bench.py's roofline bookkeeping for the configs[3] legs (CPU only): the
-algorithmic bytes the resolution claim kernel is charged per candidate in
-each table form (csrc/resolution.hip: packed one-word keys up to 31
-variables, clause indices beyond), and which kernel the roofline names."""
+"""bench.py's roofline bookkeeping for the configs[3] legs (CPU only).
+
+* php-res: the fused pass kernel (csrc/resolution.hip res_pass_packed_kernel)
+  is charged against the issue pipe its SQ passes found binding
+  (profiles/sq_issue.json "php-res_B1", per step) over the run's live kernel
+  time, with the step's HBM bytes beside it;
+* php-dp: a solve is a chain of dependent launches, priced against one launch
+  per the shortest kernel of the trace (bench.DP_MIN_KERNEL_US)."""
 import bench
 
 
-def _stats(claim_ms, pair_ms):
-    return [{"candidates": 1000, "pairs": 5000, "claim_ms": claim_ms, "pair_ms": pair_ms}] * 2
+def _res_stats(pair_ms):
+    return [{"candidates": 1000, "pairs": 5000, "claim_ms": 0.0, "pair_ms": pair_ms}] * 2
 
 
-def test_claim_kernel_bytes_per_candidate():
-    packed = bench.saturation_roofline(_stats(2.0, 1.0), nvars=12)
-    index = bench.saturation_roofline(_stats(2.0, 1.0), nvars=40)
-    assert packed["kernel"].startswith("ht_cand_packed_kernel")
-    assert index["kernel"].startswith("ht_cand_kernel")
-    # K = 2 words: key 16 B + slot read/CAS 16 B + flag 8 B; index form adds the
-    # occupant key 16 B and the slot 8 B
-    assert packed["algorithmic_bytes_per_step"] == 1000 * 40
-    assert index["algorithmic_bytes_per_step"] == 1000 * 64
-    assert abs(packed["achieved"] - 40e3 / 2e-3 / 1e9) < 1e-12
-    assert packed["frac"] == packed["achieved"] / bench.HBM_PEAK_GBS
-
-
-def test_pair_kernel_named_when_it_dominates():
-    r = bench.saturation_roofline(_stats(0.5, 1.5), nvars=12)
-    assert r["kernel"] == "res_pairs_kernel"
-    assert r["algorithmic_bytes_per_step"] == 5000 * 16 + 1000 * 16
+def test_saturation_roofline_is_the_issue_roofline_of_the_pass_kernel():
+    e = bench.load_profile("sq_issue.json", "php-res_B1")
+    assert e, "profiles/sq_issue.json lacks the php-res entry"
+    r = bench.saturation_roofline(_res_stats(0.25), nvars=12)
+    assert r["kernel"].startswith("res_pass_packed_kernel")
+    issue = bench.issue_roofline("php-res", 1, 0.25, kernel="res")
+    for k in ("bound", "achieved", "peak", "frac", "unit"):
+        assert r[k] == issue[k], k
+    # the pipe fraction is the profiled instruction count over this run's time
+    cyc = e["effective_clock_hz"] * 0.25e-3
+    peaks = {"valu": 1024 * 0.5 * cyc, "salu": 256 * cyc, "lds": 256 * cyc}
+    counts = {"valu": e["valu_insts"], "salu": e["salu_insts"], "lds": e["lds_array_cycles"]}
+    assert abs(r["frac"] - counts[r["bound"]] / peaks[r["bound"]]) < 1e-12
+    assert r["kernel_ms_per_step"] == 0.25
+    assert r["pairs_per_step"] == 5000 and r["candidates_per_step"] == 1000
+    assert r["hbm_bytes_per_step"] == e.get("hbm_bytes_corrected")
     assert bench.saturation_roofline([], nvars=12) is None
+
+
+def test_dp_roofline_prices_the_launch_chain():
+    st = [{"launches": 280, "device_ms": 3.0, "subset_tests": 10, "new_clauses": 4, "words": 2}] * 3
+    r = bench.dp_roofline(st, solves_per_s=300.0)
+    assert r["bound"] == "launch-latency" and r["unit"] == "launches/s"
+    assert r["achieved"] == 280 * 300.0
+    assert r["peak"] == 1e6 / bench.DP_MIN_KERNEL_US
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    assert abs(r["us_per_launch"] - 3.0e3 / 280) < 1e-9
+    assert bench.dp_roofline([], 1.0) is None
