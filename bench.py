@@ -60,6 +60,7 @@ from satmi.shard import gather_verdicts, shard_range  # noqa: E402
 
 METRIC = "instances solved/sec, random 3-SAT n=100 α=4.26; unit-props/sec; HBM GB/s"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_CLOCK_HZ = 2.4e9          # MI355X peak engine clock (MI355X_MICROARCH.md: "2.4 GHz" issue rates)
 SHADER_CLOCK_HZ = 2.4e9        # MI355X_MICROARCH.md: peak engine clock (the LDS-issue peak of dp_roofline)
 CHUNK = 4096                   # instances per generation chunk (chunk c drawn from seed + c)
 FIX_NCAP, FIX_MCAP = 127, 448  # dpll_fixed_kernel's shape class (csrc/dpll_scan.hip)
@@ -230,13 +231,16 @@ def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll"):
     """The DPLL kernel's binding resource is inside the CU: issue-pipe fractions
     from the SQ counter passes kept in profiles/sq_issue.json (tools/sq_roofline.py:
     wave-instructions / LDS-array cycles per launch of this exact workload) over
-    this run's live kernel time at the profiled effective clock.  Peaks: VALU 0.5
+    this run's live kernel time at the peak engine clock.  Peaks: VALU 0.5
     wave-instructions / cycle / SIMD, SALU 1 / cycle / CU, LDS array 1 cycle /
     cycle / CU.  `stale` if the kernel source changed since the profile."""
     e = load_profile("sq_issue.json", f"{preset}_B{per_gpu}")
     if not e:
         return None
-    cyc = e["effective_clock_hz"] * kernel_ms * 1e-3
+    # the pipes' peak at the chip's peak engine clock (a short profiled kernel's
+    # GRBM_GUI_ACTIVE-derived clock is not its live clock; a long one's, e.g.
+    # the headline kernel's 2.39 GHz, is within 1 % of the peak)
+    cyc = PEAK_CLOCK_HZ * kernel_ms * 1e-3
     pipes = {"valu": (e["valu_insts"], 1024 * 0.5 * cyc, "wave-instr"),
              "salu": (e["salu_insts"], 256 * cyc, "instr"),
              "lds": (e["lds_array_cycles"], 256 * cyc, "array-cycles")}
@@ -246,7 +250,8 @@ def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll"):
     return {"bound": bound, "achieved": a / (kernel_ms * 1e-3), "peak": p / (kernel_ms * 1e-3),
             "unit": unit + "/s", "frac": fr[bound], "fracs": fr,
             "lds_bank_conflict_share": e["lds_bank_conflict_cycles"] / e["lds_array_cycles"],
-            "clock_hz": e["effective_clock_hz"], "source": e["source"], "kernel": e.get("kernel"),
+            "clock_hz": PEAK_CLOCK_HZ, "profile_clock_hz": e["effective_clock_hz"], "source": e["source"],
+            "kernel": e.get("kernel"),
             "stale": e["kernel_src_sha256_16"] != kernel_src_sha(kernel)}
 
 
