@@ -274,23 +274,40 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
     if (lds_fp)
         for (int d = tid; d < V; d += POP_THREADS) fp_sh[d] = A.firstpos[d];
     __syncthreads();
-    // rank the variables by first position (positions are distinct)
-    int live = 0;
+    // the variables that occur: their count and range
+    int live = 0, vmax = 0, vlow = 0;   // vlow: INT32_MAX - the smallest
     for (int d = tid; d < V; d += POP_THREADS) {
         const unsigned long long f = lds_fp ? fp_sh[d] : A.firstpos[d];
         if (f == ~0ull) continue;
         ++live;
-        int rank = 0;
-        for (int e = 0; e < V; ++e) rank += (lds_fp ? fp_sh[e] : A.firstpos[e]) < f ? 1 : 0;
-        (lds_fp ? ord_sh : A.order)[rank] = A.d2v[d];
+        const int32_t v = A.d2v[d];
+        vmax = max(vmax, v);
+        vlow = max(vlow, INT32_MAX - v);
     }
     const int nv = block_sum(live, wsum);
+    vmax = block_max(vmax, wsum);
+    const int32_t vmin = INT32_MAX - block_max(vlow, wsum);
+    // every variable below the set's final table size: pop() is the smallest
+    // (pyset_dev.h py_size_after); otherwise the set is built in insertion order
+    const bool small_ints = nv > 0 && (int64_t)vmax < py_size_after(nv);
+    if (!small_ints) {   // rank the variables by first position (positions are distinct)
+        for (int d = tid; d < V; d += POP_THREADS) {
+            const unsigned long long f = lds_fp ? fp_sh[d] : A.firstpos[d];
+            if (f == ~0ull) continue;
+            int rank = 0;
+            for (int e = 0; e < V; ++e) rank += (lds_fp ? fp_sh[e] : A.firstpos[e]) < f ? 1 : 0;
+            (lds_fp ? ord_sh : A.order)[rank] = A.d2v[d];
+        }
+        __syncthreads();
+    }
     if (tid == 0) {
         int32_t popped = 0;
         if (nv == 0) {   // `while variables` ends: True (REF.py:130)
             S->result = 1;
             S->done = 1;
             sh_quit = 1;
+        } else if (small_ints) {
+            popped = vmin;
         } else {
             // the model set in LDS when it fits (a chain of dependent probes)
             DSet s;
@@ -309,16 +326,16 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
                         break;
                     }
             }
-            if (!sh_quit && A.step_limit > 0 && S->steps >= A.step_limit) {
-                S->result = -1;
-                S->done = 1;
-                sh_quit = 1;
-            }
-            if (!sh_quit && A.limit_ticks && __builtin_amdgcn_s_memrealtime() - S->t0 > A.limit_ticks) {
-                S->result = -1;
-                S->done = 1;
-                sh_quit = 1;
-            }
+        }
+        if (!sh_quit && A.step_limit > 0 && S->steps >= A.step_limit) {
+            S->result = -1;
+            S->done = 1;
+            sh_quit = 1;
+        }
+        if (!sh_quit && A.limit_ticks && __builtin_amdgcn_s_memrealtime() - S->t0 > A.limit_ticks) {
+            S->result = -1;
+            S->done = 1;
+            sh_quit = 1;
         }
         sh_var = popped;
     }

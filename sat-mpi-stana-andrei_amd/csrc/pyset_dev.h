@@ -57,6 +57,24 @@ __device__ __forceinline__ void dset_init(DSet &s, int32_t *a, int32_t *b, int64
 
 __device__ __forceinline__ DView dset_view(const DSet &s) { return {s.t, s.mask, s.fill, s.used}; }
 
+// The table size of a fresh set after n distinct adds (no deletions, so fill
+// == used): set_add_entry resizes when fill * 5 >= mask * 3, to the smallest
+// power of two > used * 4 (used * 2 past 50,000).  When every element is a
+// small int below that size, each sits at its own slot (distinct home slots
+// never collide), so the table is the elements in increasing order whatever
+// the insertion order -- and a fresh set's pop() returns the smallest.
+__host__ __device__ __forceinline__ int64_t py_size_after(int64_t n) {
+    int64_t mask = PY_MINSIZE - 1;
+    for (;;) {
+        const int64_t thr = (mask * 3 + 4) / 5;   // the fill that triggers the next resize
+        if (n < thr) return mask + 1;
+        const int64_t minused = thr > 50000 ? thr * 2 : thr * 4;
+        int64_t ns = PY_MINSIZE;
+        while (ns <= minused) ns <<= 1;
+        mask = ns - 1;
+    }
+}
+
 __device__ void py_insert_clean(int32_t *table, uint64_t mask, int32_t key) {
     const int64_t h = py_hash(key);
     uint64_t perturb = (uint64_t)h;
