@@ -305,6 +305,7 @@ struct ResState {
     int64_t passes;
     int64_t pairs, candidates;    // whole saturation
     int64_t stripe_max;           // the last pass's largest stripe count (sizes a regrown stage)
+    uint64_t tk_pass, pass_ticks; // the running pass kernel's start tick; pass kernel ticks summed
     uint64_t t0;                  // s_memrealtime at the start
     int32_t done, result, empty, timeout, overflow;
     int32_t spill;                // the pass's new keys outgrew the stage: counted, not stored
@@ -414,6 +415,10 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
     __shared__ unsigned long long abase;
     ResState *S = A.st;
     if (S->done) return;
+    // the kernel's duration on the device clock: from its first block's start
+    // to the next kernel's (res_gather_kernel) -- no events, so it also works
+    // inside the replayed graph
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) S->tk_pass = __builtin_amdgcn_s_memrealtime();
     const int64_t jlo = S->jlo, ncl = S->ncl;
     const uint64_t t0 = S->t0;
     const int ln = lane_id(), tid = threadIdx.x;
@@ -526,6 +531,8 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
 __global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
     __shared__ int64_t pre[RES_STRIPES + 1];
     ResState *S = A.st;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && !S->done)
+        S->pass_ticks += __builtin_amdgcn_s_memrealtime() - S->tk_pass;
     if (S->done || S->overflow) return;
     if (S->spill) {   // the stage held a part of the pass's keys: the host regrows it and runs the pass again
         if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
@@ -728,6 +735,27 @@ struct EventTimer {
 // stream), and the number of workspaces is the peak number of concurrent
 // calls.  A saturation of a small formula is a few passes of small launches,
 // so allocating its buffers per call cost more than its kernels.
+// The packed path's first segment of a call (state init, key packing, table
+// seeding, the first batch of passes, the state's copy back), captured into a
+// HIP graph the second time the same segment is enqueued and replayed from
+// then on: one launch instead of ~16 host submissions, whose gaps were a
+// quarter of a php-res call.  Keyed by everything its launches read from the
+// host.
+struct ResGraph {
+    hipGraphExec_t exec = nullptr;
+    ResArgs args;
+    int64_t ncl = -1;
+    const void *clauses = nullptr;
+    uint64_t tslots = 0;
+    int batch = 0;
+    ResGraph() { std::memset(&args, 0, sizeof(args)); }
+    void reset() {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        exec = nullptr;
+        ncl = -1;
+    }
+};
+
 struct ResWork {
     DevBuf clauses, cand, counters, table, flag, pos, slotv, tiles, grand;
     DevBuf keys, state, passnew, stage, stripes;   // the packed path
@@ -738,7 +766,9 @@ struct ResWork {
     unsigned long long *pin = nullptr;   // pinned host words: the per-chunk counters and claim count
     ResState *pst = nullptr;             // pinned host copy of the packed path's state
     int dev = 0;
+    ResGraph graph;
     ~ResWork() {   // only a workspace that failed part-way is destroyed (after its stream drained)
+        graph.reset();
         if (stream) (void)hipStreamDestroy(stream);
         if (pin) (void)hipHostFree(pin);
         if (pst) (void)hipHostFree(pst);
@@ -868,14 +898,6 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     };
     uint64_t tslots = slots_for(key_cap);
     SATMI_TRY(wk.table.reserve(8 * tslots));
-    // the state and the stripes set on the device (no copies from the host),
-    // then the keys packed; the deadline is measured from the pack kernel's
-    // start (t0 written by it; no clauses: no pairs, the deadline is never read)
-    hipLaunchKernelGGL(res_init_kernel, dim3(1), dim3(2 * RES_STRIPES), 0, s, wk.state.as<ResState>(),
-                       (int64_t)nclauses, wk.stripes.as<unsigned long long>(), slot_base);
-    if (nclauses > 0)
-        hipLaunchKernelGGL(res_pack_kernel, dim3(grid_for(nclauses)), dim3(256), 0, s, wk.clauses.as<uint64_t>(),
-                           (int64_t)nclauses, wk.keys.as<uint64_t>(), wk.state.as<ResState>());
     ResState &st = *wk.pst;   // the host's copy, refreshed after each batch of passes
     st = ResState{};
     st.ncl = nclauses;
@@ -889,10 +911,22 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         SATMI_HIP(hipGetLastError());
         return SATMI_OK;
     };
-    SATMI_TRY(seed(nclauses));
+    // the state and the stripes set on the device (no copies from the host),
+    // then the keys packed; the deadline is measured from the pack kernel's
+    // start (t0 written by it; no clauses: no pairs, the deadline is never read)
+    const auto prologue = [&]() -> int {
+        hipLaunchKernelGGL(res_init_kernel, dim3(1), dim3(2 * RES_STRIPES), 0, s, wk.state.as<ResState>(),
+                           (int64_t)nclauses, wk.stripes.as<unsigned long long>(), slot_base);
+        if (nclauses > 0)
+            hipLaunchKernelGGL(res_pack_kernel, dim3(grid_for(nclauses)), dim3(256), 0, s,
+                               wk.clauses.as<uint64_t>(), (int64_t)nclauses, wk.keys.as<uint64_t>(),
+                               wk.state.as<ResState>());
+        return seed(nclauses);
+    };
     double hz = 1e8;
     (void)satmi_wallclock_hz(&hz);
     ResArgs A;
+    std::memset(&A, 0, sizeof(A));   // padding too: the first segment's graph is keyed by these bytes
     const auto args = [&]() {
         A.st = wk.state.as<ResState>();
         A.keys = wk.keys.as<uint64_t>();
@@ -910,27 +944,59 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         A.stripes = wk.stripes.as<unsigned long long>();
     };
     args();
-    EventTimer &t_pairs = wk.t_pairs;
-    t_pairs.reset();
     g_stats = ResStats{};
     const bool record = h_rec_lits && h_rec_clause_off && h_rec_pass_off;
     int64_t rec_clauses = 0, rec_lits = 0;
     std::vector<uint64_t> hkeys;
     const dim3 pass_grid(256, 32);   // j-tiles x i-tiles, grid-stride
-    for (;;) {
-        // passes per wait: all of them when the count is bounded (<= 16)
-        const int64_t left = max_passes > 0 ? max_passes - st.passes : 4;
-        const int batch = record ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(left, 16));
-        const int64_t ncl_before = st.ncl;
+    const auto passes = [&](int batch) -> int {   // a batch of passes, then the state back
         for (int b = 0; b < batch; ++b) {
-            t_pairs.begin(s);
             hipLaunchKernelGGL(res_pass_packed_kernel, pass_grid, dim3(256), 0, s, A);
-            t_pairs.end(s);
             hipLaunchKernelGGL(res_gather_kernel, dim3(8, RES_STRIPES), dim3(256), 0, s, A);
             hipLaunchKernelGGL(res_finish_pass_kernel, dim3(1), dim3(RES_STRIPES), 0, s, A);
         }
         SATMI_HIP(hipGetLastError());
         SATMI_HIP(hipMemcpyAsync(wk.pst, wk.state.p, sizeof(ResState), hipMemcpyDeviceToHost, s));
+        return SATMI_OK;
+    };
+    bool first = true;
+    for (;;) {
+        // passes per wait: all of them when the count is bounded (<= 16)
+        const int64_t left = max_passes > 0 ? max_passes - st.passes : 4;
+        const int batch = record ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(left, 16));
+        const int64_t ncl_before = st.ncl;
+        if (first) {   // the prologue and the first batch: replayed from the graph when they repeat
+            first = false;
+            ResGraph &G = wk.graph;
+            const bool same = G.ncl == nclauses && G.clauses == wk.clauses.p && G.tslots == tslots &&
+                              G.batch == batch && std::memcmp(&G.args, &A, sizeof(ResArgs)) == 0;
+            if (same && G.exec) {
+                SATMI_HIP(hipGraphLaunch(G.exec, s));
+            } else if (same) {
+                hipGraph_t graph = nullptr;
+                SATMI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+                int rc = prologue();
+                if (rc == SATMI_OK) rc = passes(batch);
+                const hipError_t ec = hipStreamEndCapture(s, &graph);
+                if (rc != SATMI_OK) return rc;
+                SATMI_HIP(ec);
+                const hipError_t ei = hipGraphInstantiate(&G.exec, graph, nullptr, nullptr, 0);
+                (void)hipGraphDestroy(graph);
+                SATMI_HIP(ei);
+                SATMI_HIP(hipGraphLaunch(G.exec, s));
+            } else {   // remember the segment: captured if it comes again
+                G.reset();
+                G.args = A;
+                G.ncl = nclauses;
+                G.clauses = wk.clauses.p;
+                G.tslots = tslots;
+                G.batch = batch;
+                SATMI_TRY(prologue());
+                SATMI_TRY(passes(batch));
+            }
+        } else {
+            SATMI_TRY(passes(batch));
+        }
         SATMI_HIP(hipStreamSynchronize(s));
         if (st.overflow) {   // grow the key buffer and / or the table, re-seed, run the pass again
             if (time_limit_s > 0 &&
@@ -983,7 +1049,7 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     *h_passes = (int32_t)st.passes;
     g_stats.pairs = st.pairs;
     g_stats.candidates = st.candidates;
-    g_stats.pair_ms = t_pairs.total();
+    g_stats.pair_ms = (double)st.pass_ticks / hz * 1e3;   // device clock, pass kernels only
     g_stats.claim_ms = 0.0;   // fused into the pass kernel
     return SATMI_OK;
 }
