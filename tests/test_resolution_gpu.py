@@ -81,6 +81,29 @@ def test_pigeonhole_php43_four_passes(golden_dir):
             assert r["clauses"][k] == p["clauses"], k
 
 
+def test_repeated_calls_replay_the_captured_segment(golden_dir):
+    """A call's first segment (state init, packing, seeding, the first batch of
+    passes) is captured into a HIP graph the second time it repeats and
+    replayed after (csrc/resolution.hip ResGraph): the bench's php-res call
+    five times in a row, with other formulas in between (a new key: the
+    segment is re-captured), adds the reference's sets every time."""
+    with open(os.path.join(golden_dir, "resolution_php43.json")) as fh:
+        (c,) = json.load(fh)["cases"]
+    f = cnf.pigeonhole(3)
+    want = [p["count"] for p in c["passes"]]
+    for k in range(5):
+        r = resolve(f, max_passes=4, record=k == 4)
+        assert r["result"] == -1 and r["pass_new"] == want, k
+        if k == 2:   # another formula in between, twice (captured on its second call)
+            g = cnf.pigeonhole(2)
+            o = oracle.resolution(g)
+            for _ in range(2):
+                rg = resolve(g)
+                assert (rg["result"], rg["pass_new"]) == (o["result"], o["pass_new"])
+    for k, p in enumerate(c["passes"]):   # the last call recorded its sets
+        assert clause_set_sha(r["clauses"][k]) == p["sha256"], k
+
+
 @pytest.mark.parametrize("base", [(1 << 31) - 37, (1 << 32) - 50])
 def test_append_slots_past_2_31(base):
     """The pair kernel's candidate slots start at `base` (test knob): the first
