@@ -1360,8 +1360,12 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
             int rc = SATMI_OK;
             for (int k = 0; k < batch && rc == SATMI_OK; ++k) rc = enqueue_step(A);
             const hipError_t ec = hipStreamEndCapture(s, &graph);
-            if (rc != SATMI_OK) return rc;
-            SATMI_HIP(ec);
+            if (rc != SATMI_OK || ec != hipSuccess) {
+                if (graph) (void)hipGraphDestroy(graph);
+                G.reset();
+                if (rc != SATMI_OK) return rc;
+                SATMI_HIP(ec);
+            }
             const hipError_t ei = hipGraphInstantiate(&G.exec, graph, nullptr, nullptr, 0);
             (void)hipGraphDestroy(graph);
             SATMI_HIP(ei);

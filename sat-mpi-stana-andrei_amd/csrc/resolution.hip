@@ -978,8 +978,12 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
                 int rc = prologue();
                 if (rc == SATMI_OK) rc = passes(batch);
                 const hipError_t ec = hipStreamEndCapture(s, &graph);
-                if (rc != SATMI_OK) return rc;
-                SATMI_HIP(ec);
+                if (rc != SATMI_OK || ec != hipSuccess) {
+                    if (graph) (void)hipGraphDestroy(graph);
+                    G.reset();
+                    if (rc != SATMI_OK) return rc;
+                    SATMI_HIP(ec);
+                }
                 const hipError_t ei = hipGraphInstantiate(&G.exec, graph, nullptr, nullptr, 0);
                 (void)hipGraphDestroy(graph);
                 SATMI_HIP(ei);
