@@ -70,6 +70,7 @@ def main():
             "lds": c["SQ_LDS_IDX_ACTIVE"] / (CUS * cyc),
         },
         "source": keep or src,
+        "kernel": bench.get("roofline", {}).get("kernel"),   # the launch's kernel as the bench line names it
     }
     try:
         with open(OUT) as fh:
