@@ -24,7 +24,7 @@ def eliminate(formula, step_limit=0, clause_limit=0, time_limit=0.0, record=Fals
     L = _capi.load()
     _capi.require_gpu()
     off, lits = _csr(formula)
-    nv = max([abs(int(l)) for c in formula for l in c] + [1])
+    nv = max(int(np.abs(lits.astype(np.int64)).max()) if len(formula) and off[-1] else 1, 1)
     res = ctypes.c_int32(0)
     steps = ctypes.c_int32(0)
     trace = np.zeros(nv + 1, dtype=np.int32)

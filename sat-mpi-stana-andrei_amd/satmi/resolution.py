@@ -5,6 +5,7 @@ plus, optionally, the set of clauses each pass added; `resolution_solve` is the
 reference's boolean entry point.
 """
 import ctypes
+import itertools
 
 import numpy as np
 
@@ -16,13 +17,18 @@ class ResolutionLimit(Exception):
 
 
 def _csr(formula):
+    """The formula's CSR host arrays (clause offsets, literals), built without a
+    per-literal Python loop (a call's conversion is part of its time)."""
     off = np.zeros(len(formula) + 1, dtype=np.int32)
-    for i, c in enumerate(formula):
-        off[i + 1] = off[i] + len(c)
-    flat = [int(l) for c in formula for l in c]
-    if any(l == 0 for l in flat):
+    np.cumsum(np.fromiter(map(len, formula), dtype=np.int32, count=len(formula)), out=off[1:])
+    n = int(off[-1])
+    if n == 0:
+        return off, np.zeros(1, dtype=np.int32)
+    # (a literal outside int32 raises OverflowError here, like np.asarray did)
+    flat = np.fromiter(itertools.chain.from_iterable(formula), dtype=np.int32, count=n)
+    if not flat.all():
         raise ValueError("literal 0 is not allowed (REF.py:51)")
-    return off, np.asarray(flat or [0], dtype=np.int32)
+    return off, flat
 
 
 def _p(a, t=ctypes.c_int32):
