@@ -52,11 +52,13 @@ namespace {
 #ifdef SATMI_PHASE_STAMPS
 struct PhaseClock {
     uint64_t acc[8];
+    uint64_t cnt[8];   // path counts (written after the clocks)
     uint64_t t;
     __device__ void start() {
-        for (int i = 0; i < 8; ++i) acc[i] = 0;
+        for (int i = 0; i < 8; ++i) acc[i] = cnt[i] = 0;
         t = __builtin_amdgcn_s_memtime();
     }
+    __device__ void count(int i, uint64_t v = 1) { cnt[i] += v; }
     __device__ void mark(int i) {
         const uint64_t x = __builtin_amdgcn_s_memtime();
         acc[i] += x - t;
@@ -67,6 +69,7 @@ struct PhaseClock {
 struct PhaseClock {
     __device__ void start() {}
     __device__ void mark(int) {}
+    __device__ void count(int, uint64_t = 1) {}
 };
 #endif
 enum { PH_STAGE = 0, PH_ASSIGN = 1, PH_UNITS = 2, PH_CONFLICT = 3, PH_COUNTS = 4, PH_CHOOSE = 5, PH_PURE = 6,
@@ -327,9 +330,12 @@ constexpr int FAST_UNITS = 8;
 constexpr int FAST_BATCH = 16;
 
 template <int K, typename C>
-__device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t ep, uint32_t bep, int *empty_at) {
+__device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t ep, uint32_t bep, int *empty_at,
+                         PhaseClock &ph) {
     using W = typename Pack<K>::W;
     const int ln = lane_id();
+    ph.count(0);
+    ph.count(7, (uint64_t)(tl - rs));
     // fast path: a batch of at most FAST_BATCH literals (lanes 0..15; larger
     // batches are rare and take the general path below)
     if (__builtin_expect(tl - rs <= FAST_BATCH, 1)) {
@@ -345,6 +351,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
         const int delta = ob - excl;
         const int total = __builtin_amdgcn_readlane(incl, 15);
         if (__builtin_expect(total <= 64, 1)) {
+            ph.count(1);
             // one touched clause per lane
             int d = __builtin_amdgcn_readlane(delta, 0);
             if (tl - rs > 1)   // one batch literal: lane 0's list is the whole range
@@ -362,6 +369,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const uint32_t sv = valid ? clause_sum<K>(x) : 0xFFu;
             const bool empty = sv == 0u;
             if (__builtin_expect(__ballot(empty) != 0ull, 0)) {
+                ph.count(2);
                 const int et = emptier<K>(S, w, bep);   // every lane: no exec-mask branch
                 const int e = empty ? et : INT_MAX;
                 *empty_at = wave_min_i32(e);
@@ -371,7 +379,9 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const bool unit = sv == 1u;
             const uint64_t um = __ballot(unit);
             const int nun = __popcll(um);
+            ph.count(4, (uint64_t)nun);
             if (__builtin_expect(nun <= FAST_UNITS, 1)) {
+                ph.count(3);
                 // a clause reached from two batch literals is one snapshot entry
                 bool dup = false;
                 uint64_t dm = um;
@@ -401,8 +411,37 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 wave_sync();
                 return __popcll(dm);
             }
+            // more units than the register ranking takes: the touched clauses
+            // are already in the lanes (one step), so they are placed in clause
+            // order through the bitmap right here, not scanned again below (a
+            // clause reached from two batch literals sets one bit; its lanes
+            // write the same snapshot entry and stamp)
+            if (unit) atomicOr(&S.bm[c >> 5].x, 1u << (c & 31u));
+            wave_sync();
+            int nu = 0;
+            for (int w0 = 0; w0 < nw; w0 += 64) {
+                const int wi = w0 + ln;
+                const uint32_t bits = wi < nw ? S.bm[wi].x : 0u;
+                const int pc = __popc(bits);
+                const int in = wave_incl_scan(pc);
+                if (wi < nw) S.bm[wi].y = (uint32_t)(nu + in - pc);
+                nu += lane63(in);
+            }
+            wave_sync();
+            if (unit) {
+                const uint2 pb = S.bm[c >> 5];
+                const uint32_t k = pb.y + (uint32_t)__popc(pb.x & ((1u << (c & 31u)) - 1u));
+                const uint32_t code = unit_code<K>(w, x);
+                S.snap[k] = (C)code;
+                ts_stamp(S, code >> 1, stamp(ep, k));
+            }
+            wave_sync();
+            for (int wi = ln; wi < nw; wi += 64) S.bm[wi].x = 0u;   // clean bitmap for the next round
+            ph.count(6);
+            return nu;
         }
     }
+    ph.count(5);
     int e = INT_MAX;
     int passes = 0;
     bool unit = false;          // this lane found a unit clause (valid when one pass covered all touched clauses)
@@ -553,7 +592,7 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
         wave_sync();
         ph.mark(PH_ASSIGN);
         const int nassign = tl - rs;
-        const int nu_next = INC ? inc_units<K>(S, (mpad + 31) >> 5, rs, tl, ++ep, bep, &e)
+        const int nu_next = INC ? inc_units<K>(S, (mpad + 31) >> 5, rs, tl, ++ep, bep, &e, ph)
                                 : scan_units<K>(S, mpad, ++ep, bep, &e);
         ph.mark(PH_UNITS);
         if (__builtin_expect(e != INT_MAX, 0)) break;
@@ -1410,8 +1449,8 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     }
 #ifdef SATMI_PHASE_STAMPS
     ph.mark(PH_OTHER);
-    if (!is_task && A.root_lits && A.sol_stride >= 16 && ln < 8)
-        ((int64_t *)(A.root_lits + (int64_t)b * A.sol_stride))[ln] = (int64_t)ph.acc[ln];
+    if (!is_task && A.root_lits && A.sol_stride >= 32 && ln < 16)
+        ((int64_t *)(A.root_lits + (int64_t)b * A.sol_stride))[ln] = (int64_t)(ln < 8 ? ph.acc[ln] : ph.cnt[ln - 8]);
 #endif
     if (SPLIT && nd > 0) cancel_donations(A, dst, nd);   // a model (or a cancellation) came first
     flush_counters(ctr, c, flushed);
