@@ -52,10 +52,11 @@ namespace {
 #ifdef SATMI_PHASE_STAMPS
 struct PhaseClock {
     uint64_t acc[8];
-    uint64_t cnt[8];   // path counts (written after the clocks)
+    uint64_t cnt[16];   // path counts (written after the clocks)
     uint64_t t;
     __device__ void start() {
-        for (int i = 0; i < 8; ++i) acc[i] = cnt[i] = 0;
+        for (int i = 0; i < 8; ++i) acc[i] = 0;
+        for (int i = 0; i < 16; ++i) cnt[i] = 0;
         t = __builtin_amdgcn_s_memtime();
     }
     __device__ void count(int i, uint64_t v = 1) { cnt[i] += v; }
@@ -380,6 +381,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const uint64_t um = __ballot(unit);
             const int nun = __popcll(um);
             ph.count(4, (uint64_t)nun);
+            ph.count(nun == 0 ? 10 : nun == 1 ? 11 : nun == 2 ? 12 : nun <= FAST_UNITS ? 13 : 6, nun <= FAST_UNITS ? 1 : 0);
             if (__builtin_expect(nun <= FAST_UNITS, 1)) {
                 ph.count(3);
                 // a clause reached from two batch literals is one snapshot entry
@@ -442,6 +444,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
         }
     }
     ph.count(5);
+    ph.count(tl - rs > FAST_BATCH ? 8 : 9);
     int e = INT_MAX;
     int passes = 0;
     bool unit = false;          // this lane found a unit clause (valid when one pass covered all touched clauses)
@@ -565,12 +568,14 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
     // the decision literal (the first batch's first entry, always assigned or
     // kept) is not a propagation in REF.py's counters: taken off once here
     props -= dec ? 1u : 0u;
+    ph.count(14);
     while (nu > 0) {
         ++rounds;
         rs = tl;
         const uint32_t bep = ep;   // the batch's epoch
         int k0 = 0;
         do {   // nu > 0: at least one step
+            ph.count(15);
             const int k = k0 + ln;
             // lanes past nu read entry 0 (its variable is stamped with index 0
             // != k: never first).  Stale entries past nu are not safe to read:
@@ -1449,7 +1454,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     }
 #ifdef SATMI_PHASE_STAMPS
     ph.mark(PH_OTHER);
-    if (!is_task && A.root_lits && A.sol_stride >= 32 && ln < 16)
+    if (!is_task && A.root_lits && A.sol_stride >= 48 && ln < 24)
         ((int64_t *)(A.root_lits + (int64_t)b * A.sol_stride))[ln] = (int64_t)(ln < 8 ? ph.acc[ln] : ph.cnt[ln - 8]);
 #endif
     if (SPLIT && nd > 0) cancel_donations(A, dst, nd);   // a model (or a cancellation) came first

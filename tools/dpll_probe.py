@@ -43,7 +43,7 @@ def main():
     ctr = torch.zeros((B, 8), dtype=torch.int64, device=dev)
     sl = torch.zeros(B, dtype=torch.int32, device=dev)
     so = torch.zeros((B, max(n, 16)), dtype=torch.int32, device=dev)
-    stride = max(n, 32)
+    stride = max(n, 48)
     root_len = torch.zeros(B, dtype=torch.int32, device=dev)
     root = torch.zeros((B, stride), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev)
@@ -82,11 +82,12 @@ def main():
             out["cycles_per_node"] = {nm: float(ph[i]) / nodes for i, nm in enumerate(names)}
             out["cycles_per_node"]["total"] = float(ph.sum()) / nodes
             out["rounds_per_node"] = float(c[:, 6].sum()) / nodes
-            if kern in (_capi.KERNEL_SCAN, _capi.KERNEL_INC) and root.shape[1] >= 32:
+            if kern in (_capi.KERNEL_SCAN, _capi.KERNEL_INC) and root.shape[1] >= 48:
                 # path counts of the incremental unit scan (csrc/dpll_scan.hip inc_units, diag build)
-                cn = root[:, :32].cpu().contiguous().view(torch.int64)[:, 8:16].double().sum(0)
+                cn = root[:, :48].cpu().contiguous().view(torch.int64)[:, 8:24].double().sum(0)
                 cnames = ("unit_scans", "fast_one_step", "fast_conflict", "fast_few_units", "units_found",
-                          "general", "unused", "batch_literals")
+                          "general", "fast_bitmap", "batch_literals", "general_batch_gt16", "general_touched_gt64",
+                          "fast_nun0", "fast_nun1", "fast_nun2", "fast_nun3_8", "propagate_calls", "assign_steps")
                 out["per_node"] = {nm: float(cn[i]) / nodes for i, nm in enumerate(cnames)}
         print(json.dumps(out), flush=True)
 
