@@ -324,10 +324,11 @@ __device__ __forceinline__ int emptier(const SLds<K, C> &S, typename Pack<K>::W 
     return tt;
 }
 
-// Unit clauses in a round whose touched clauses fit one wave step and that
-// found at most this many of them: ranked in clause order by register
-// comparisons (no bitmap round trips through LDS).
-constexpr int FAST_UNITS = 8;
+// A round whose touched clauses fit one wave step ranks at most two unit
+// clauses by register comparisons; more go through the clause bitmap, which
+// measured faster than ranking 3-8 units by readlane loops
+// (profiles/r04/steps/dpll_fast_units_threshold_ab.txt).
+constexpr int FAST_UNITS = 2;
 constexpr int FAST_BATCH = 16;
 
 template <int K, typename C>
@@ -381,29 +382,20 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             const uint64_t um = __ballot(unit);
             const int nun = __popcll(um);
             ph.count(4, (uint64_t)nun);
-            ph.count(nun == 0 ? 10 : nun == 1 ? 11 : nun == 2 ? 12 : nun <= FAST_UNITS ? 13 : 6, nun <= FAST_UNITS ? 1 : 0);
+            ph.count(nun == 0 ? 10 : nun == 1 ? 11 : nun == 2 ? 12 : nun <= 8 ? 13 : 6, nun <= 8 ? 1 : 0);
             if (__builtin_expect(nun <= FAST_UNITS, 1)) {
                 ph.count(3);
                 // a clause reached from two batch literals is one snapshot entry
                 bool dup = false;
                 uint64_t dm = um;
                 int rank = 0;
-                if (nun == 2) {   // the commonest case, without loops: lanes u0 < u1
+                if (nun == 2) {   // lanes u0 < u1 (one unit: snapshot index 0)
                     const int u0 = __builtin_ctzll(um), u1 = 63 - __builtin_clzll(um);
                     const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)c, u0);
                     const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)c, u1);
                     dup = (ln == u1) & (c0 == c1);
                     dm = c0 == c1 ? 1ull << u0 : um;   // a duplicate keeps lane u0 only
                     rank = ln == u0 ? (c1 < c0 ? 1 : 0) : (c0 < c1 ? 1 : 0);
-                } else if (nun > 1) {   // one unit: no duplicate, snapshot index 0
-                    for (uint64_t r = um; r; r &= r - 1) {
-                        const int u = __builtin_ctzll(r);
-                        const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)c, u);
-                        dup |= (u < ln) & (cu == c);   // no short circuit: no exec-mask branch
-                    }
-                    dm = __ballot(unit && !dup);
-                    for (uint64_t r = dm; r; r &= r - 1)
-                        rank += (uint32_t)__builtin_amdgcn_readlane((int)c, __builtin_ctzll(r)) < c ? 1 : 0;
                 }
                 if (unit && !dup) {
                     const uint32_t code = unit_code<K>(w, x);
