@@ -413,6 +413,13 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             if (unit) atomicOr(&S.bm[c >> 5].x, 1u << (c & 31u));
             wave_sync();
             int nu = 0;
+            if (nw <= 64) {   // up to 2,048 clauses: one prefix scan
+                const uint32_t bits = ln < nw ? S.bm[ln].x : 0u;
+                const int pc = __popc(bits);
+                const int in = wave_incl_scan(pc);
+                if (ln < nw) S.bm[ln].y = (uint32_t)(in - pc);
+                nu = lane63(in);
+            } else
             for (int w0 = 0; w0 < nw; w0 += 64) {
                 const int wi = w0 + ln;
                 const uint32_t bits = wi < nw ? S.bm[wi].x : 0u;
@@ -428,9 +435,12 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 const uint32_t code = unit_code<K>(w, x);
                 S.snap[k] = (C)code;
                 ts_stamp(S, code >> 1, stamp(ep, k));
+                // clean bitmap for the next round: only the words units set (a
+                // wave's LDS operations run in order, so every lane of the word
+                // has read it above)
+                S.bm[c >> 5].x = 0u;
             }
             wave_sync();
-            for (int wi = ln; wi < nw; wi += 64) S.bm[wi].x = 0u;   // clean bitmap for the next round
             ph.count(6);
             return nu;
         }
