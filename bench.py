@@ -114,7 +114,7 @@ def parse(argv=None):
                    help="DPLL kernel policy (satmi_dpll_set_kernel); auto = incremental clause kernel")
     p.add_argument("--no-split", action="store_true", help="disable branch splitting (satmi_dpll_set_split)")
     p.add_argument("--split-always", action="store_true",
-                   help="split every eligible launch (default: 1 to 8 instances per resident wave)")
+                   help="split every eligible launch (default: at least 1 and fewer than 4 instances per resident wave)")
     p.add_argument("--split-warmup", type=int, default=-1,
                    help="nodes before a search may donate (satmi_dpll_set_split_warmup; -1 = default)")
     p.add_argument("--helpers-per-cu", type=int, default=0, help="branch-splitting helpers per CU (0 = library default)")
@@ -485,7 +485,9 @@ def run_dpll(args, world, rank, local):
         "config": {"workload": desc, "preset": args.workload, "node_limit": args.node_limit,
                    "instances_per_step": args.total, "instances_per_gpu": B, "n": n, "m": m, "k": k,
                    "parallelism": f"instance-sharded x{world}", "streams": NS,
-                   "branch_splitting": not args.no_split},
+                   "branch_splitting": not args.no_split,
+                   "split_policy": "off" if args.no_split else "always" if args.split_always else "auto",
+                   "helpers_per_cu": args.helpers_per_cu or 1, "split_warmup": args.split_warmup},
         "instances_per_s": all_inst / elapsed,
         "unit_props_per_s": props / elapsed,
         "capped_fraction": int(((status == 2).sum()).item()) / B,

@@ -258,7 +258,7 @@ int satmi_dpll_set_kernel(int policy);
  * cancelled and count nothing).  Applies to SOUND-mode launches with
  * max_solutions == 1, no node limit and no time limit.
  *   enable          0 off; 1 auto (default): launches with at least one and
- *                   fewer than 8 instances per resident wavefront; 2 every
+ *                   fewer than 4 instances per resident wavefront; 2 every
  *                   eligible launch
  *   helpers_per_cu  wavefronts per CU that stay as helpers once the queue
  *                   drains (0 = default 1); the others exit, freeing their CU

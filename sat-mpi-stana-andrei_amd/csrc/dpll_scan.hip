@@ -981,7 +981,7 @@ static_assert(sizeof(SplitCfg) == SPLIT_POOL_OFF, "SplitCfg layout");
 // existing event test (next_event), so the split form's loop carries no
 // per-decision counter: what it keeps live is only read at the checks.
 constexpr uint32_t SPLIT_CHECK_NODES = 16u;
-constexpr int SPLIT_MAX_PER_WAVE = 8;   // split a launch only below this many instances per resident wave
+constexpr int SPLIT_MAX_PER_WAVE = 4;   // split a launch only below this many instances per resident wave (r05 sweep: profiles/r05/n8share.json)
 // Kernels come in two forms: SPLIT = false has no branch-splitting code at all
 // (its register cost -- SGPR spills in the node loop -- was measured at ~4 % of
 // the full-size rate), SPLIT = true can split.  The host launches the split
