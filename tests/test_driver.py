@@ -82,3 +82,49 @@ def test_scripted_menu_session(tmp_path):
     assert "Found 1 solution(s)" in text
     assert "CDCL            Error        " in text   # a failing solver is reported as an error row
     assert printed[-1] == "Exiting program."
+
+
+def _pipe_fixture(golden_dir):
+    import json
+    with open(os.path.join(golden_dir, "driver_pipe.json")) as fh:
+        return json.load(fh)
+
+
+def test_large_results_time_out_like_the_reference_queue(golden_dir):
+    """REF.py:417-431 joins its solver child before draining the result queue,
+    so a result whose pickle does not fit the pipe reads as a timeout there.
+    Pinned by running the reference's own execute_with_timeout
+    (tests/golden/make_golden_pipe.py): the exact byte boundary on stub
+    results, and REF-mode DPLL results (here from the oracle, REF.py:133-214)
+    either side of it -- same pickled size, same outcome."""
+    import oracle
+    fx = _pipe_fixture(golden_dir)
+    assert driver.pipe_capacity() == fx["pipe_buffer_bytes"]
+    assert any(c["outcome"] == "result" for c in fx["stub_cases"])
+    assert any(c["outcome"] != "result" for c in fx["stub_cases"])
+    for c in fx["stub_cases"]:
+        got = driver.execute_with_timeout(lambda f, n=c["string_len"]: "x" * n, [[1]], 60)
+        want = ("x" * c["string_len"], None) if c["outcome"] == "result" else (None, "Timeout after 60 seconds")
+        assert got == want, c["payload_bytes"]
+    outcomes = set()
+    for c in fx["cases"]:
+        sols = oracle.dpll(c["formula"], "ref")["solutions"]
+        result = [{abs(l): l > 0 for l in s} for s in sols]
+        assert len(result) == c["solutions"]
+        got = driver.execute_with_timeout(lambda f: result, c["formula"], 60)
+        if c["outcome"] == "result":
+            assert got == (result, None)
+        else:
+            assert got == (None, c["outcome"].format(timeout=60))
+        from multiprocessing.reduction import ForkingPickler
+        assert len(ForkingPickler.dumps(("result", result))) == c["payload_bytes"]
+        outcomes.add(c["outcome"])
+    assert len(outcomes) == 2
+    # the opt-out returns the result itself
+    big = [{i: True} for i in range(1, 20001)]
+    driver.REFERENCE_PIPE_LIMIT = False
+    try:
+        assert driver.execute_with_timeout(lambda f: big, [[1]], 60) == (big, None)
+    finally:
+        driver.REFERENCE_PIPE_LIMIT = True
+    assert driver.execute_with_timeout(lambda f: big, [[1]], 60) == (None, "Timeout after 60 seconds")

@@ -46,3 +46,22 @@ def test_menu_large_formula_times_out_like_reference():
     for name in ("DPLL", "Hybrid"):
         assert results[name]["output"] == "Timeout after 2 seconds", results[name]
         assert results[name]["time"] == 2
+
+
+def test_large_results_time_out_like_the_reference_queue_on_gpu(golden_dir):
+    """The GPU dpll_optimized through the driver: results the reference's
+    result pipe cannot carry read as its timeout, the others come back whole
+    (tests/golden/driver_pipe.json, from REF.py's own execute_with_timeout)."""
+    import json
+    import os
+    from satmi.solvers import dpll_optimized
+    with open(os.path.join(golden_dir, "driver_pipe.json")) as fh:
+        fx = json.load(fh)
+    for c in fx["cases"]:
+        result, error = driver.execute_with_timeout(dpll_optimized, c["formula"], 60)
+        if c["outcome"] == "result":
+            assert error is None and len(result) == c["solutions"], c["shape"]
+            sols = oracle.dpll(c["formula"], "ref")["solutions"]
+            assert result == [{abs(l): l > 0 for l in s} for s in sols]
+        else:
+            assert (result, error) == (None, c["outcome"].format(timeout=60)), c["shape"]
