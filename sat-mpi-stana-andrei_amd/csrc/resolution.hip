@@ -306,6 +306,7 @@ struct ResState {
     int64_t pairs, candidates;    // whole saturation
     int64_t stripe_max;           // the last pass's largest stripe count (sizes a regrown stage)
     uint64_t tk_pass, pass_ticks; // the running pass kernel's start tick; pass kernel ticks summed
+    uint64_t tk_last;             // the last pass kernel's ticks (added by finish_pass unless the pass overflowed)
     uint64_t t0;                  // s_memrealtime at the start
     int32_t done, result, empty, timeout, overflow;
     int32_t spill;                // the pass's new keys outgrew the stage: counted, not stored
@@ -532,7 +533,7 @@ __global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
     __shared__ int64_t pre[RES_STRIPES + 1];
     ResState *S = A.st;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && !S->done)
-        S->pass_ticks += __builtin_amdgcn_s_memrealtime() - S->tk_pass;
+        S->tk_last = __builtin_amdgcn_s_memrealtime() - S->tk_pass;
     if (S->done || S->overflow) return;
     if (S->spill) {   // the stage held a part of the pass's keys: the host regrows it and runs the pass again
         if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
@@ -560,11 +561,13 @@ __global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
 }
 
 // the verdict of a pass with nnew new clauses, or the next pass's bounds
-__device__ void finish_pass(const ResArgs &A, ResState *S, int64_t nnew) {
-    if (S->overflow) {   // the host grows the buffers and runs this pass again
+__device__ void finish_pass(const ResArgs &A, ResState *S, int64_t nnew, int64_t cands) {
+    if (S->overflow) {   // the host grows the buffers and runs this pass again (its work and time count then)
         S->done = 1;
         return;
     }
+    S->candidates += cands;
+    S->pass_ticks += S->tk_last;
     S->pairs += (S->ncl * (S->ncl - 1) - S->jlo * (S->jlo - 1)) / 2;
     if (S->empty) {   // an empty resolvent: unsatisfiable (REF.py:84-85)
         S->result = 0;
@@ -609,8 +612,7 @@ __global__ void __launch_bounds__(RES_STRIPES) res_finish_pass_kernel(ResArgs A)
     if (S->done) return;
     S->stripe_max = smax;
     S->count = (unsigned long long)claims;   // this pass's claims (a regrowth is sized by them)
-    S->candidates += cands;
-    finish_pass(A, S, claims);
+    finish_pass(A, S, claims, cands);
 }
 
 // ------------------------------------------------------------------ host side
@@ -881,7 +883,7 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
                       int rec_pass_cap) {
     hipStream_t s = wk.stream;
     const auto t_call = std::chrono::steady_clock::now();
-    const int PCAP = 1 << 12;   // passes whose counts the device keeps (the host copies out pass_cap of them)
+    const int PCAP = std::max(1, std::min(pass_cap, 1 << 16));   // passes whose counts the device keeps
     SATMI_TRY(wk.keys.reserve(8 * (size_t)std::max<int64_t>(4 * (int64_t)nclauses, 1 << 14)));
     SATMI_TRY(wk.state.reserve(sizeof(ResState)));
     SATMI_TRY(wk.passnew.reserve(8 * (size_t)PCAP));

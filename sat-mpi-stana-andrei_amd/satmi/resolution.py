@@ -44,7 +44,7 @@ def resolve(formula, max_passes=0, clause_limit=0, time_limit=0.0, record=False,
     res = ctypes.c_int32(0)
     passes = ctypes.c_int32(0)
     pcap = int(max_passes) if 0 < max_passes < (1 << 16) else 1 << 16
-    pass_new = np.empty(pcap, dtype=np.int64)   # (the first `passes` entries are written)
+    pass_new = np.zeros(pcap, dtype=np.int64)
     if record:
         rl = np.zeros(rec_cap, dtype=np.int32)
         rco = np.zeros(rec_cap + 1, dtype=np.int64)

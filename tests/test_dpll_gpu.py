@@ -414,12 +414,15 @@ def test_bench_kernel_matches_reference_fixture(golden_dir, tag, split):
         assert r.solutions(b) == want, (tag, b)
 
 
-@pytest.mark.parametrize("n,m,cap", [(200, 700, 800), (300, 1100, 500)])
+@pytest.mark.parametrize("n,m,cap", [(200, 700, 800), (300, 1100, 500), (500, 2130, 400), (480, 2400, 400)])
 def test_scan_kernel_chunk_group_tails(n, m, cap):
     """Clause counts whose 64-clause chunks split into a 7-chunk group followed
     by a 4-chunk group (m=700: 11 chunks; m=1100: 7+7+4 = 18 chunks) -- the
-    for_chunks path of dpll_scan.hip no other shape reaches.  Scan kernel vs
-    general kernel vs oracle, node-capped, every counter and any model."""
+    for_chunks path of dpll_scan.hip no other shape reaches -- and 3-SAT with
+    more than 2,048 clauses (m=2130, 2400: unit bitmaps of 67 / 75 words, the
+    multi-word placement loop of the one-step unit scan's bitmap path, ADVICE
+    r04).  Scan kernel vs general kernel vs oracle, node-capped, every counter
+    and any model."""
     batch = cnf.uniform_ksat(6, n, m, 3, seed=n + m)
     rg = _run_policy(batch, _capi.KERNEL_GENERAL, max_solutions=1, node_limit=cap, sol_cap=1)
     ri = _run_policy(batch, _capi.KERNEL_INC, max_solutions=1, node_limit=cap, sol_cap=1)

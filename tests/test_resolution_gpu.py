@@ -181,3 +181,44 @@ def test_candidate_buffer_rerun_path():
     assert r["result"] == o["result"] and r["pass_new"] == o["pass_new"]
     assert [sorted(p) for p in r["clauses"]] == [sorted(p) for p in o["clauses"]]
 
+
+
+def test_graph_replay_alternating_formulas_of_one_shape():
+    """the captured segment is keyed by clause count, buffers,
+    table size and argument bytes, not by the clauses.  Two different formulas
+    with the same clause count and variable count (<= 31: the packed path),
+    alternated so both are captured and replayed several times, must each add
+    their own clause sets every call (a replay reads the newly encoded clauses)."""
+    rng = random.Random(55)
+    nv, m = 9, 14
+    fs = []
+    while len(fs) < 2:
+        f = [sorted(rng.sample(range(1, nv + 1), 3)) for _ in range(m)]
+        f = [[v if rng.random() < 0.5 else -v for v in c] for c in f]
+        if len({abs(l) for c in f for l in c}) == nv and f not in fs:
+            fs.append(f)
+    want = [oracle.resolution(f, record=True, max_passes=3) for f in fs]
+    assert want[0]["pass_new"] != want[1]["pass_new"] or want[0]["clauses"] != want[1]["clauses"]
+    for k in range(8):
+        i = k % 2
+        r = resolve(fs[i], max_passes=3, record=True)
+        assert (r["result"], r["pass_new"]) == (want[i]["result"], want[i]["pass_new"]), (k, i)
+        assert [sorted(p) for p in r["clauses"]] == [sorted(p) for p in want[i]["clauses"]], (k, i)
+
+
+def test_regrowth_call_reports_each_pass_once():
+    """a pass stopped by an overflow runs again on regrown
+    buffers; its candidates and kernel time count once.  A call on fresh
+    (trimmed) workspaces regrows during PHP(4,3)'s 4th pass; its statistics
+    equal those of the next call, which needs no regrowth."""
+    from satmi import _capi
+    from satmi.resolution import last_stats
+    f = cnf.pigeonhole(3)
+    _capi.trim_workspaces()
+    r1 = resolve(f, max_passes=4)
+    s1 = last_stats()
+    r2 = resolve(f, max_passes=4)
+    s2 = last_stats()
+    assert r1 == r2
+    assert (s1["pairs"], s1["candidates"]) == (s2["pairs"], s2["candidates"])
+    assert s1["pair_ms"] < 1.6 * s2["pair_ms"] + 0.05
