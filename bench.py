@@ -86,6 +86,10 @@ LEGS = [
     ("configs[3] php-res", "php-res", ["--steps", "20", "--warmup", "2"]),
     ("configs[4] uf250", "uf250", ["--steps", "4", "--warmup", "1"]),
     ("configs[4] 5sat-n200", "5sat-n200", ["--steps", "4", "--warmup", "1"]),
+    # configs[4] solved to the end (no node limit): 512 uf250-shaped searches per
+    # step, branch splitting on with helper waves on every other CU slot
+    ("configs[4] uf250 solved", "uf250", ["--node-limit", "0", "--total", "512", "--split-always",
+                                          "--helpers-per-cu", "10", "--steps", "2", "--warmup", "0"]),
     ("cdcl", "cdcl", ["--steps", "3", "--warmup", "1"]),
     ("cdcl 4 threads", "cdcl", ["--steps", "3", "--warmup", "1", "--threads", "4"]),
 ]
@@ -106,6 +110,8 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=20251016)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-node-limit", type=int, default=2000,
+                   help="searches solved to the end: the CPU sample's node cap (its rate scaled to instances/s)")
     p.add_argument("--no-legs", action="store_true", help="only the headline workload (no `configs` object)")
     p.add_argument("--legs-only", action="store_true", help=argparse.SUPPRESS)   # the child of the default run
     p.add_argument("--leg-cpu-seconds", type=float, default=4.0, help="CPU baseline budget of each leg")
@@ -174,12 +180,27 @@ def cpu_pool(kind, icb, clb, lits, seconds, param):
     return json.loads(out.stdout.strip().splitlines()[-1]), cores
 
 
-def cpu_baseline(batch_host, seconds, node_limit):
+def cpu_baseline(batch_host, seconds, node_limit, props_per_instance=None, sample_node_limit=0):
     """The CPU oracle (oracle/, a C restatement of REF.py's DPLL, SOUND mode) on
     rank 0's host, on the same bench batch: one core (instances from the start
     of the batch until `seconds` / 3 pass), then every core (oracle/cpu_pool.py,
     one worker per core, for `seconds`).  `value` is the all-cores rate; the
-    one-core rate is beside it."""
+    one-core rate is beside it.
+
+    Searches solved to the end (node_limit 0) with sample_node_limit > 0: one
+    uf250-shaped search is ~10^3 s of one host core (the oracle runs ~6 k
+    nodes/s there), so no bounded sample finishes one.  The sample is then the
+    same instances node-capped at sample_node_limit, and its unit-props/s is
+    scaled to instances/s by the unit propagations per instance of the GPU's
+    full solves of the same batch (bit-exact counters: the same searches)."""
+    if node_limit == 0 and sample_node_limit > 0 and props_per_instance:
+        r = cpu_baseline(batch_host, seconds, sample_node_limit)
+        ups = r["unit_props_per_s"]
+        r.update({"value": ups / props_per_instance, "unit": "instances/s", "scaled_from": "unit-props/s",
+                  "props_per_instance": props_per_instance,
+                  "sample": r["sample"] + f"; scaled to instances/s by {props_per_instance:.4g} unit propagations "
+                            f"per instance solved to the end (the GPU's counters on this batch)"})
+        return r
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -452,11 +473,15 @@ def run_dpll(args, world, rank, local):
     workload = f"dpll_sound_{k}sat_n{n}_a{args.alpha}_B{B}"
     # resident waves of the persistent grid -> how busy the waves were (tail of the batch)
     kern, lds, per_cu = _capi.plan(n, m, m * k, k)
-    resident = min(B, torch.cuda.get_device_properties(dev).multi_processor_count * per_cu)
-    # busy wave-time over resident wave-time of the timed region (all streams)
-    util = ticks / world / hz / (resident * elapsed)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     st = _capi.split_stats(streams[last].cuda_stream) if not args.no_split else {"done": 0}
     split_used = bool(st["done"])
+    # a splitting launch of a batch smaller than the CU slots adds helper waves
+    # (csrc/dpll_scan.hip dpll_scan_launch): they count as resident
+    extra = ncu * (args.helpers_per_cu or 1) if split_used else 0
+    resident = min(B + extra, ncu * per_cu)
+    # busy wave-time over resident wave-time of the timed region (all streams)
+    util = ticks / world / hz / (resident * elapsed)
     pmc = load_profile("pmc_traffic.json", workload)
     kname = dpll_kernel_name(n, m, k, split_used)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -743,7 +768,9 @@ def run_one(args, world, rank, local):
     if args.workload in CDCL:
         return run_cdcl(args, world, rank, local)
     out, host = run_dpll(args, world, rank, local)
-    out["cpu_baseline"] = cpu_baseline(host, args.cpu_seconds, args.node_limit) if host is not None else None
+    ppi = out["unit_props_per_s"] / out["instances_per_s"] if out["instances_per_s"] else None
+    out["cpu_baseline"] = (cpu_baseline(host, args.cpu_seconds, args.node_limit, ppi, args.cpu_sample_node_limit)
+                           if host is not None else None)
     return out
 
 
@@ -759,7 +786,7 @@ def legs_main(args):
         keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_issue",
                 "cpu_baseline", "result", "passes_or_steps", "instances_per_s", "unit_props_per_s",
                 "capped_fraction", "sat_fraction", "sat", "unsat", "iteration_capped", "iterations_per_s",
-                "verdict_sha", "kernel_ms", "wave_utilisation", "oracle_check")
+                "verdict_sha", "kernel_ms", "wave_utilisation", "oracle_check", "resident_waves", "branch_split")
         out[name] = {k: r[k] for k in keep if k in r}
         out[name]["leg_wall_s"] = time.perf_counter() - t
     print(json.dumps(out), flush=True)

@@ -1819,7 +1819,7 @@ int dpll_scan_launch(const ScanLaunch &L) {
     const int waves_per_wg = P.waves_per_wg;
     const uint32_t wg_lds = lay.bytes * (uint32_t)waves_per_wg;
     const int need = (L.num_instances + waves_per_wg - 1) / waves_per_wg;
-    const int grid = std::max(1, std::min(need, L.num_cus * P.wg_per_cu));
+    int grid = std::max(1, std::min(need, L.num_cus * P.wg_per_cu));
 
     ScanArgs A;
     A.inst_clause_begin = L.inst_clause_begin;
@@ -1863,6 +1863,13 @@ int dpll_scan_launch(const ScanLaunch &L) {
         cfg.dstack_cap = ncap + 1;
         cfg.max_helpers = L.num_cus * L.split_helpers_per_cu;
         cfg.warm = (uint32_t)std::max(L.split_warmup, 0);
+        // a batch smaller than the resident slots (split always: configs[4]
+        // solved to the end) gets its helpers from the start: waves beyond the
+        // instances find the queue empty and register as helpers at once, so
+        // the hard searches' subtrees spread over idle CU slots instead of
+        // waiting for the easy instances to finish
+        const int64_t with_helpers = ((int64_t)L.num_instances + cfg.max_helpers + waves_per_wg - 1) / waves_per_wg;
+        grid = (int)std::max<int64_t>(grid, std::min<int64_t>(with_helpers, (int64_t)L.num_cus * P.wg_per_cu));
         const size_t pool = (size_t)cfg.slot_cap * (size_t)cfg.slot_bytes;
         const size_t stacks = (size_t)grid * (size_t)waves_per_wg * (size_t)cfg.dstack_cap * sizeof(int32_t);
         uint32_t epoch = 0;
