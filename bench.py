@@ -196,6 +196,7 @@ def cpu_baseline(batch_host, seconds, node_limit, props_per_instance=None, sampl
     if node_limit == 0 and sample_node_limit > 0 and props_per_instance:
         r = cpu_baseline(batch_host, seconds, sample_node_limit)
         ups = r["unit_props_per_s"]
+        r["sample_capped_instances_per_s"] = r.pop("instances_per_s")
         r.update({"value": ups / props_per_instance, "unit": "instances/s", "scaled_from": "unit-props/s",
                   "props_per_instance": props_per_instance,
                   "sample": r["sample"] + f"; scaled to instances/s by {props_per_instance:.4g} unit propagations "
