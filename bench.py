@@ -249,7 +249,7 @@ def kernel_src_sha(kernel="dpll"):
         return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
-def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll"):
+def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll", clock_hz=None):
     """The DPLL kernel's binding resource is inside the CU: issue-pipe fractions
     from the SQ counter passes kept in profiles/sq_issue.json (tools/sq_roofline.py:
     wave-instructions / LDS-array cycles per launch of this exact workload) over
@@ -261,8 +261,11 @@ def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll"):
         return None
     # the pipes' peak at the chip's peak engine clock (a short profiled kernel's
     # GRBM_GUI_ACTIVE-derived clock is not its live clock; a long one's, e.g.
-    # the headline kernel's 2.39 GHz, is within 1 % of the peak)
-    cyc = PEAK_CLOCK_HZ * kernel_ms * 1e-3
+    # the headline kernel's 2.39 GHz, is within 1 % of the peak), or at the
+    # live clock the kernel measured itself (clock_hz: s_memtime over
+    # s_memrealtime inside the kernel), with the peak-clock fractions beside it
+    hz = clock_hz or PEAK_CLOCK_HZ
+    cyc = hz * kernel_ms * 1e-3
     pipes = {"valu": (e["valu_insts"], 1024 * 0.5 * cyc, "wave-instr"),
              "salu": (e["salu_insts"], 256 * cyc, "instr"),
              "lds": (e["lds_array_cycles"], 256 * cyc, "array-cycles")}
@@ -271,8 +274,10 @@ def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll"):
     a, p, unit = pipes[bound]
     return {"bound": bound, "achieved": a / (kernel_ms * 1e-3), "peak": p / (kernel_ms * 1e-3),
             "unit": unit + "/s", "frac": fr[bound], "fracs": fr,
+            "fracs_at_peak_clock": {k: v * hz / PEAK_CLOCK_HZ for k, v in fr.items()},
             "lds_bank_conflict_share": e["lds_bank_conflict_cycles"] / e["lds_array_cycles"],
-            "clock_hz": PEAK_CLOCK_HZ, "profile_clock_hz": e["effective_clock_hz"], "source": e["source"],
+            "clock_hz": hz, "clock_source": "live (in-kernel s_memtime / s_memrealtime)" if clock_hz else "peak",
+            "profile_clock_hz": e["effective_clock_hz"], "source": e["source"],
             "kernel": e.get("kernel"),
             "stale": e["kernel_src_sha256_16"] != kernel_src_sha(kernel)}
 
@@ -573,7 +578,9 @@ def saturation_roofline(stats, nvars):
     if not stats:
         return None
     pms = sum(s["pair_ms"] for s in stats) / len(stats)
-    roof = issue_roofline("php-res", 1, pms, kernel="res")
+    clocks = sorted(s["shader_clock_hz"] for s in stats if s.get("shader_clock_hz"))
+    live_hz = clocks[len(clocks) // 2] if clocks else None   # median over the timed calls
+    roof = issue_roofline("php-res", 1, pms, kernel="res", clock_hz=live_hz)
     if roof is None:
         return None
     e = load_profile("sq_issue.json", "php-res_B1") or {}

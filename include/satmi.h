@@ -138,6 +138,13 @@ int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, const int32
  * launches (HIP events on its stream), for rooflines. */
 int satmi_resolution_last_stats(int64_t *pairs, int64_t *candidates, double *pair_ms, double *claim_ms);
 
+/* The live shader clock (Hz) of the last satmi_resolution_host call's fused
+ * pass kernels (at most 31 variables): shader cycles (s_memtime) over
+ * device-clock ticks (s_memrealtime) summed over one block in 64 of every
+ * pass, so an issue roofline prices the pipes at the clock the kernel ran
+ * at.  0 when no pass kernel ran (the general path beyond 31 variables). */
+int satmi_resolution_last_clock(double *shader_hz);
+
 /* Test knob: the first append slot (default 0) of the pair kernel's candidates
  * (more than 31 variables) or of a pass's new clauses (at most 31), so a small
  * pass exercises the slot arithmetic past 2^31 / 2^32. */

@@ -307,6 +307,8 @@ struct ResState {
     int64_t stripe_max;           // the last pass's largest stripe count (sizes a regrown stage)
     uint64_t tk_pass, pass_ticks; // the running pass kernel's start tick; pass kernel ticks summed
     uint64_t tk_last;             // the last pass kernel's ticks (added by finish_pass unless the pass overflowed)
+    uint64_t clk_cyc, clk_ticks;  // sampled pass-kernel blocks: shader cycles (s_memtime) and device-clock
+                                  // ticks (s_memrealtime) summed -- the live shader clock is their ratio
     uint64_t t0;                  // s_memrealtime at the start
     int32_t done, result, empty, timeout, overflow;
     int32_t spill;                // the pass's new keys outgrew the stage: counted, not stored
@@ -424,6 +426,10 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
     const uint64_t t0 = S->t0;
     const int ln = lane_id(), tid = threadIdx.x;
     const int stripe = (int)((blockIdx.y * gridDim.x + blockIdx.x) % RES_STRIPES);
+    // the live shader clock: one block in RES_STRIPES stamps both clocks around its work
+    const bool clk_sample = stripe == 0 && threadIdx.x == 0;
+    const uint64_t c_begin = clk_sample ? __builtin_amdgcn_s_memtime() : 0ull;
+    const uint64_t r_begin = clk_sample ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // tiles ~ (ncl - jlo) / tj x ncl / 512 (the triangle) ~ RES_TILES
     const int tj = (int)max<int64_t>(1, min<int64_t>(RES_TJ, (ncl - jlo) * (ncl / 512 + 1) / RES_TILES));
     int cand = 0;
@@ -525,6 +531,11 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
         tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     }
     if (tid == 0 && tot) atomicAdd(A.stripes + RES_STRIPES + stripe, (unsigned long long)tot);
+    if (clk_sample) {
+        const uint64_t dc = __builtin_amdgcn_s_memtime() - c_begin, dr = __builtin_amdgcn_s_memrealtime() - r_begin;
+        atomicAdd((unsigned long long *)&S->clk_cyc, (unsigned long long)dc);
+        atomicAdd((unsigned long long *)&S->clk_ticks, (unsigned long long)dr);
+    }
 }
 
 // the pass's new keys, packed from the stripe regions after the clause list
@@ -696,6 +707,7 @@ size_t g_cand_bytes = CAND_BYTES;   // test knob: the candidate buffer's cap (fo
 struct ResStats {
     int64_t pairs = 0, candidates = 0, keys_tabled = 0;
     double pair_ms = 0.0, claim_ms = 0.0;
+    double shader_hz = 0.0;   // the pass kernels' live shader clock (packed path; 0 = not sampled)
 };
 thread_local ResStats g_stats;   // the calling thread's last call
 
@@ -1057,6 +1069,7 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     g_stats.candidates = st.candidates;
     g_stats.pair_ms = (double)st.pass_ticks / hz * 1e3;   // device clock, pass kernels only
     g_stats.claim_ms = 0.0;   // fused into the pass kernel
+    g_stats.shader_hz = st.clk_ticks ? (double)st.clk_cyc / (double)st.clk_ticks * hz : 0.0;
     return SATMI_OK;
 }
 
@@ -1071,6 +1084,15 @@ extern "C" int satmi_resolution_last_stats(int64_t *pairs, int64_t *candidates, 
     if (candidates) *candidates = g_stats.candidates;
     if (pair_ms) *pair_ms = g_stats.pair_ms;
     if (claim_ms) *claim_ms = g_stats.claim_ms;
+    return SATMI_OK;
+}
+
+extern "C" int satmi_resolution_last_clock(double *shader_hz) {
+    if (!shader_hz) {
+        set_error("satmi_resolution_last_clock: null pointer");
+        return SATMI_ERR_ARG;
+    }
+    *shader_hz = g_stats.shader_hz;
     return SATMI_OK;
 }
 

@@ -29,7 +29,8 @@ EXPORTED = (
     "satmi_dpll_batch_device", "satmi_dpll_batch_host", "satmi_dpll_lds_bytes", "satmi_resolution_host",
     "satmi_dp_host", "satmi_dpll_scan_lds_bytes", "satmi_dpll_set_kernel", "satmi_dpll_plan",
     "satmi_dpll_launch_span", "satmi_wallclock_hz", "satmi_resolution_debug_slot_base",
-    "satmi_resolution_last_stats", "satmi_dpll_set_split", "satmi_dpll_split_stats", "satmi_dp_last_stats",
+    "satmi_resolution_last_stats", "satmi_resolution_last_clock", "satmi_dpll_set_split", "satmi_dpll_split_stats",
+    "satmi_dp_last_stats",
     "satmi_cdcl_batch_host", "satmi_dpll_set_split_warmup", "satmi_resolution_debug_cand_bytes",
     "satmi_dp_trim", "satmi_resolution_trim", "satmi_cdcl_last_stats",
 )
@@ -133,6 +134,7 @@ def load():
                                         P(ctypes.c_double)]
     L.satmi_resolution_last_stats.argtypes = [i64p, i64p, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)]
+    L.satmi_resolution_last_clock.argtypes = [ctypes.POINTER(ctypes.c_double)]
     L.satmi_dp_host.argtypes = [
         ctypes.c_int, i32p, i32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, i32p, i32p, ctypes.c_int, i32p,
         i32p, ctypes.c_int64, i64p, ctypes.c_int64, i64p, ctypes.c_int]

@@ -68,13 +68,17 @@ def resolve(formula, max_passes=0, clause_limit=0, time_limit=0.0, record=False,
 
 def last_stats():
     """Work and device time of the last resolve() call: pairs, candidate
-    resolvents, pair-kernel ms and claim (hash dedup) kernel ms."""
+    resolvents, pair-kernel ms, claim (hash dedup) kernel ms, and the pass
+    kernels' live shader clock (Hz; 0 on the general path)."""
     L = _capi.load()
     pairs, cand = ctypes.c_int64(0), ctypes.c_int64(0)
     pms, cms = ctypes.c_double(0.0), ctypes.c_double(0.0)
     _capi.check(L.satmi_resolution_last_stats(ctypes.byref(pairs), ctypes.byref(cand), ctypes.byref(pms),
                                               ctypes.byref(cms)), "satmi_resolution_last_stats")
-    return {"pairs": pairs.value, "candidates": cand.value, "pair_ms": pms.value, "claim_ms": cms.value}
+    hz = ctypes.c_double(0.0)
+    _capi.check(L.satmi_resolution_last_clock(ctypes.byref(hz)), "satmi_resolution_last_clock")
+    return {"pairs": pairs.value, "candidates": cand.value, "pair_ms": pms.value, "claim_ms": cms.value,
+            "shader_clock_hz": hz.value}
 
 
 def resolution_solve(formula, time_limit=0.0):

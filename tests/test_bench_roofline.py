@@ -41,3 +41,18 @@ def test_dp_roofline_prices_the_launch_chain():
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
     assert abs(r["us_per_launch"] - 3.0e3 / 280) < 1e-9
     assert bench.dp_roofline([], 1.0) is None
+
+
+def test_saturation_roofline_prices_the_pipes_at_the_live_clock():
+    """The pass kernels measure their own shader clock (s_memtime over
+    s_memrealtime, satmi_resolution_last_clock): the roofline's pipe peaks
+    are priced at the median live clock of the timed calls, with the
+    peak-clock fractions beside it."""
+    st = [dict(s, shader_clock_hz=hz) for s, hz in zip(_res_stats(0.25) * 2, (1.2e9, 1.4e9, 1.3e9, 1.3e9))]
+    r = bench.saturation_roofline(st, nvars=12)
+    assert r["clock_hz"] == 1.3e9 and r["clock_source"].startswith("live")
+    peak = bench.saturation_roofline(_res_stats(0.25), nvars=12)
+    assert peak["clock_source"] == "peak" and peak["clock_hz"] == bench.PEAK_CLOCK_HZ
+    for k, v in r["fracs"].items():
+        assert abs(v * 1.3e9 / bench.PEAK_CLOCK_HZ - peak["fracs"][k]) < 1e-12
+        assert abs(r["fracs_at_peak_clock"][k] - peak["fracs"][k]) < 1e-12
