@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstddef>
@@ -334,30 +335,18 @@ struct ResArgs {
     unsigned long long *stripes;     // [RES_STRIPES] append counts (from slot_base), [RES_STRIPES] candidates
 };
 constexpr int RES_STRIPES = 64;
+// words after the stripes' 2 x RES_STRIPES counters, each group on its own 128-B line
+constexpr int RES_CLK = 2 * RES_STRIPES;         // [RES_CLK], [RES_CLK + 1]: sampled shader cycles, device ticks
+constexpr int RES_GDONE = 2 * RES_STRIPES + 16;  // gather blocks finished with the current pass
+constexpr int RES_STRIPE_WORDS = 2 * RES_STRIPES + 32;
+constexpr int RES_DONE_WORD = RES_STRIPE_WORDS;  // the last batch's S->done for the conditional reset (not reset)
+constexpr int RES_STRIPE_ALLOC = RES_STRIPE_WORDS + 16;
 
 // A probe run of this many full buckets means the table is filling up (at
 // load <= 1/2 it practically never happens): the pass stops as an overflow and
 // runs again on a larger table -- instead of probing a full table for ever.
 constexpr int RES_PROBE_MAX = 32;
 constexpr int RES_BUCKET = 8;             // slots per bucket: one 64-B read checks them all
-
-// a saturation's starting state and append stripes (one block of 2 x RES_STRIPES threads)
-__global__ void res_init_kernel(ResState *S, int64_t ncl, unsigned long long *stripes, int64_t slot_base) {
-    const int t = threadIdx.x;
-    if (t < 2 * RES_STRIPES) stripes[t] = t < RES_STRIPES ? (unsigned long long)slot_base : 0ull;
-    if (t == 0) {
-        ResState z{};
-        z.ncl = ncl;
-        z.result = -1;
-        *S = z;
-    }
-}
-
-__global__ void __launch_bounds__(256) res_pack_kernel(const uint64_t *k2, int64_t n, uint64_t *keys, ResState *S) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) S->t0 = __builtin_amdgcn_s_memrealtime();
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
-        keys[c] = pack_key(k2 + 2 * c);
-}
 
 // Claim key r in a bucketed linear-probing table (slot order: bucket b's 8
 // slots, then bucket b+1's, ...; a key sits before the first empty slot of
@@ -396,6 +385,66 @@ __global__ void __launch_bounds__(256) res_seed_kernel(uint64_t *table, uint64_t
                                                        int64_t c0, int64_t c1, ResState *S) {
     for (int64_t c = c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < c1; c += (int64_t)gridDim.x * blockDim.x)
         if (bucket_claim(table, bmask, keys[c]) < 0) S->overflow = 1;
+}
+
+// The packed path's clean slate, enqueued when a call ends (and before a
+// workspace's first call): the table emptied, the state and the stripes' words
+// set for the next saturation.  It runs while the host returns the result, so
+// the next call starts with one prologue launch instead of four.
+__global__ void __launch_bounds__(256) res_reset_kernel(uint64_t *table, uint64_t tslots, ResState *S,
+                                                        unsigned long long *stripes, int64_t slot_base, int cond) {
+    // cond: only when the batch before ended the saturation (res_copyout_kernel's word)
+    if (cond && stripes[RES_DONE_WORD] == 0ull) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tslots; i += (uint64_t)gridDim.x * blockDim.x)
+        table[i] = HT_EMPTY;
+    if (blockIdx.x == 0) {
+        const int t = threadIdx.x;
+        if (t < RES_STRIPE_WORDS) stripes[t] = t < RES_STRIPES ? (unsigned long long)slot_base : 0ull;
+        if (t == 0) {
+            ResState z{};
+            z.result = -1;
+            *S = z;
+        }
+    }
+}
+
+// A batch's state and per-pass counts (`bytes`, a multiple of 4) into pinned
+// host memory, then the flag the host spins on (a stream wait wakes the host
+// ~20 us after the work ends); S->done kept for the reset that follows.
+__global__ void __launch_bounds__(64) res_copyout_kernel(const unsigned char *src, uint32_t bytes, unsigned char *dst,
+                                                         uint32_t *flag, unsigned long long *stripes) {
+    for (uint32_t i = threadIdx.x * 4u; i < bytes; i += 64u * 4u) *(uint32_t *)(dst + i) = *(const uint32_t *)(src + i);
+    if (threadIdx.x == 0) stripes[RES_DONE_WORD] = (unsigned long long)((const ResState *)src)->done;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A call's prologue (table clean, state reset): clause c's key P | N << 32
+// from the CSR literals (REF.py:66's clause sets: a repeated literal is one
+// bit), into keys[c] and the table (an input clause equal to an earlier one
+// stays out of the table, as the reference's `seen` set); the state's clause
+// count and the deadline's start.
+__global__ void __launch_bounds__(256) res_prologue_kernel(int nclauses, const int32_t *off, const int32_t *lits,
+                                                           const int32_t *var2dense, uint64_t *keys, uint64_t *table,
+                                                           uint64_t bmask, ResState *S) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        S->ncl = nclauses;
+        S->t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nclauses; c += gridDim.x * blockDim.x) {
+        uint32_t P = 0u, N = 0u;
+        for (int j = off[c]; j < off[c + 1]; ++j) {
+            const int x = lits[j];
+            const uint32_t bit = 1u << var2dense[x < 0 ? -x : x];
+            P |= x < 0 ? 0u : bit;
+            N |= x < 0 ? bit : 0u;
+        }
+        const uint64_t k = (uint64_t)P | ((uint64_t)N << 32);
+        keys[c] = k;
+        if (bucket_claim(table, bmask, k) < 0)
+            __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // One pass (REF.py:67-95) over the pairs (i < j), j in [jlo, ncl), in tiles of
@@ -533,42 +582,9 @@ __global__ void __launch_bounds__(256) res_pass_packed_kernel(ResArgs A) {
     if (tid == 0 && tot) atomicAdd(A.stripes + RES_STRIPES + stripe, (unsigned long long)tot);
     if (clk_sample) {
         const uint64_t dc = __builtin_amdgcn_s_memtime() - c_begin, dr = __builtin_amdgcn_s_memrealtime() - r_begin;
-        atomicAdd((unsigned long long *)&S->clk_cyc, (unsigned long long)dc);
-        atomicAdd((unsigned long long *)&S->clk_ticks, (unsigned long long)dr);
+        atomicAdd(A.stripes + RES_CLK, (unsigned long long)dc);   // (off the state's polled line)
+        atomicAdd(A.stripes + RES_CLK + 1, (unsigned long long)dr);
     }
-}
-
-// the pass's new keys, packed from the stripe regions after the clause list
-// (grid: x blocks per stripe, RES_STRIPES in y)
-__global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
-    __shared__ int64_t pre[RES_STRIPES + 1];
-    ResState *S = A.st;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && !S->done)
-        S->tk_last = __builtin_amdgcn_s_memrealtime() - S->tk_pass;
-    if (S->done || S->overflow) return;
-    if (S->spill) {   // the stage held a part of the pass's keys: the host regrows it and runs the pass again
-        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
-            __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    if (threadIdx.x == 0) {
-        int64_t acc = 0;
-        for (int t = 0; t < RES_STRIPES; ++t) {
-            pre[t] = acc;
-            acc += (int64_t)(A.stripes[t] - (unsigned long long)A.slot_base);
-        }
-        pre[RES_STRIPES] = acc;
-    }
-    __syncthreads();
-    const int st = blockIdx.y;
-    const int64_t ncl = S->ncl, n = pre[st + 1] - pre[st];
-    if (ncl + pre[RES_STRIPES] > A.key_cap) {   // the next clause list does not fit the key buffer
-        if (blockIdx.x == 0 && threadIdx.x == 0 && st == 0)
-            __hip_atomic_store(&S->overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
-        A.keys[ncl + pre[st] + t] = A.stage[st * A.stage_region + t];
 }
 
 // the verdict of a pass with nnew new clauses, or the next pass's bounds
@@ -602,27 +618,75 @@ __device__ void finish_pass(const ResArgs &A, ResState *S, int64_t nnew, int64_t
         S->done = 1;   // result stays -1
 }
 
-// after a pass (one workgroup of RES_STRIPES threads): the claims summed over
-// the stripes, the verdict or the next pass's bounds; the counters reset
-__global__ void __launch_bounds__(RES_STRIPES) res_finish_pass_kernel(ResArgs A) {
+// After a pass: its new keys packed from the stripe regions behind the clause
+// list (grid: x blocks per stripe, RES_STRIPES in y); then the block that
+// finishes last sums the claims over the stripes, takes the verdict or sets
+// the next pass's bounds and resets the counters -- one launch per pass
+// instead of a gather and a one-workgroup finish kernel (each launch boundary
+// was ~4.6 us of a php-res call).  The last block needs nothing the other
+// blocks wrote in this launch (the counts are the pass kernel's atomics, the
+// overflow conditions it derives itself), so the count of finished blocks is
+// a relaxed atomic with no release / acquire fences; every block has read the
+// stripes and the state before its count, so the last block may rewrite them.
+__global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
+    __shared__ int64_t pre[RES_STRIPES + 1];
     __shared__ int64_t cnt[RES_STRIPES], cand[RES_STRIPES];
+    __shared__ int sh_last;
     ResState *S = A.st;
-    const int t = threadIdx.x;
-    cnt[t] = (int64_t)(A.stripes[t] - (unsigned long long)A.slot_base);
-    cand[t] = (int64_t)A.stripes[RES_STRIPES + t];
-    A.stripes[t] = (unsigned long long)A.slot_base;
-    A.stripes[RES_STRIPES + t] = 0ull;
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && !S->done)
+        S->tk_last = __builtin_amdgcn_s_memrealtime() - S->tk_pass;
+    // S->done changes only in the last block below, after every block has
+    // read it: all blocks return here together
+    if (S->done) return;
+    const int64_t ncl = S->ncl;
+    // the pass overflowed (table), or the stage held a part of its keys: the
+    // host regrows and runs the pass again -- nothing to copy
+    const bool skip = S->overflow || S->spill;
+    if (tid == 0) {
+        int64_t acc = 0;
+        for (int t = 0; t < RES_STRIPES; ++t) {
+            pre[t] = acc;
+            acc += (int64_t)(A.stripes[t] - (unsigned long long)A.slot_base);
+        }
+        pre[RES_STRIPES] = acc;
+    }
     __syncthreads();
-    if (t != 0) return;
+    // (the next clause list must fit the key buffer)
+    if (!skip && ncl + pre[RES_STRIPES] <= A.key_cap) {
+        const int st = blockIdx.y;
+        const int64_t n = pre[st + 1] - pre[st];
+        for (int64_t t = (int64_t)blockIdx.x * blockDim.x + tid; t < n; t += (int64_t)gridDim.x * blockDim.x)
+            A.keys[ncl + pre[st] + t] = A.stage[st * A.stage_region + t];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long nb = (unsigned long long)gridDim.x * gridDim.y;
+        sh_last = __hip_atomic_fetch_add(A.stripes + RES_GDONE, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  nb - 1;
+    }
+    __syncthreads();
+    if (!sh_last) return;
+    if (tid < RES_STRIPES) {
+        cnt[tid] = (int64_t)(A.stripes[tid] - (unsigned long long)A.slot_base);
+        cand[tid] = (int64_t)A.stripes[RES_STRIPES + tid];
+        A.stripes[tid] = (unsigned long long)A.slot_base;
+        A.stripes[RES_STRIPES + tid] = 0ull;
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    A.stripes[RES_GDONE] = 0ull;
     int64_t claims = 0, cands = 0, smax = 0;
     for (int k = 0; k < RES_STRIPES; ++k) {
         claims += cnt[k];
         cands += cand[k];
         smax = max(smax, cnt[k]);
     }
-    if (S->done) return;
+    if (skip || ncl + claims > A.key_cap) S->overflow = 1;
     S->stripe_max = smax;
     S->count = (unsigned long long)claims;   // this pass's claims (a regrowth is sized by them)
+    S->clk_cyc = A.stripes[RES_CLK];
+    S->clk_ticks = A.stripes[RES_CLK + 1];
     finish_pass(A, S, claims, cands);
 }
 
@@ -667,13 +731,13 @@ struct PinBuf {
     ~PinBuf() {
         if (p) (void)hipHostFree(p);
     }
-    int reserve(size_t bytes) {
+    int reserve(size_t bytes, unsigned flags = hipHostMallocDefault) {
         if (bytes <= cap) return SATMI_OK;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
         const size_t want = std::max(bytes, (size_t)4096);
-        SATMI_HIP(hipHostMalloc((void **)&p, want, hipHostMallocDefault));
+        SATMI_HIP(hipHostMalloc((void **)&p, want, flags));
         cap = want;
         return SATMI_OK;
     }
@@ -759,9 +823,10 @@ struct ResGraph {
     hipGraphExec_t exec = nullptr;
     ResArgs args;
     int64_t ncl = -1;
-    const void *clauses = nullptr;
     uint64_t tslots = 0;
     int batch = 0;
+    const void *down = nullptr;     // non-null: the segment copies the per-pass counts back too
+    const void *pstate = nullptr;   // the pinned buffer the segment copies into
     ResGraph() { std::memset(&args, 0, sizeof(args)); }
     void reset() {
         if (exec) (void)hipGraphExecDestroy(exec);
@@ -772,20 +837,27 @@ struct ResGraph {
 
 struct ResWork {
     DevBuf clauses, cand, counters, table, flag, pos, slotv, tiles, grand;
-    DevBuf keys, state, passnew, stage, stripes;   // the packed path
+    DevBuf keys, state, stage, stripes;            // the packed path (state: ResState, then the per-pass counts)
     DevBuf up;                                     // the call's inputs (one copy from up_h)
-    PinBuf up_h, down_h;                           // pinned staging: inputs, per-pass counts
+    PinBuf up_h, pstate;                           // pinned staging: inputs; the state and counts back
+    struct Clean {   // the buffers the last reset (packed path) left clean; all null: not clean
+        const void *table = nullptr, *state = nullptr, *stripes = nullptr;
+        int64_t slot_base = -1;
+        bool operator==(const Clean &o) const {
+            return table == o.table && state == o.state && stripes == o.stripes && slot_base == o.slot_base &&
+                   table != nullptr;
+        }
+    } clean;
     EventTimer t_pairs, t_claims;
     hipStream_t stream = nullptr;
-    unsigned long long *pin = nullptr;   // pinned host words: the per-chunk counters and claim count
-    ResState *pst = nullptr;             // pinned host copy of the packed path's state
+    unsigned long long *pin = nullptr;   // pinned host words (coherent): the general path's counters and claim
+                                         // count; pin[7]: the packed path's batch flag (res_copyout_kernel)
     int dev = 0;
     ResGraph graph;
     ~ResWork() {   // only a workspace that failed part-way is destroyed (after its stream drained)
         graph.reset();
         if (stream) (void)hipStreamDestroy(stream);
         if (pin) (void)hipHostFree(pin);
-        if (pst) (void)hipHostFree(pst);
     }
 };
 
@@ -811,8 +883,7 @@ ResWork *res_acquire(int dev) {
     ResWork *w = new ResWork;
     w->dev = dev;
     if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void **)&w->pin, 64, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void **)&w->pst, sizeof(ResState), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void **)&w->pin, 64, hipHostMallocCoherent) != hipSuccess) {
         delete w;
         return nullptr;
     }
@@ -888,7 +959,12 @@ int grow_keys(ResWork &wk, int64_t want, int64_t keep, hipStream_t s) {
 // stay on the device for the whole saturation; passes are enqueued in batches
 // and the host waits once per batch (once per pass when recording).  A pass
 // that ran out of key or table room is re-run after the host grows them.
-int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t clause_limit, double time_limit_s,
+// A call is: the upload (one copy), one prologue launch (keys + table seed on
+// the table the previous call's reset left empty), the passes with the state
+// and per-pass counts back in one copy -- replayed from a HIP graph when the
+// same call repeats -- and, not waited for, the reset for the next call.
+int resolution_packed(ResWork &wk, int nclauses, const unsigned char *up, size_t o_lits, size_t o_map,
+                      int64_t max_passes, int64_t clause_limit, double time_limit_s,
                       int64_t slot_base, int V, const std::vector<int32_t> &dense2var, int32_t *h_result,
                       int32_t *h_passes, int64_t *h_pass_new, int pass_cap, int32_t *h_rec_lits,
                       int64_t rec_lit_cap, int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_pass_off,
@@ -896,10 +972,12 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     hipStream_t s = wk.stream;
     const auto t_call = std::chrono::steady_clock::now();
     const int PCAP = std::max(1, std::min(pass_cap, 1 << 16));   // passes whose counts the device keeps
+    // the state and the per-pass counts in one buffer (one copy back per batch)
+    const size_t SOFF = (sizeof(ResState) + 255) & ~(size_t)255;
     SATMI_TRY(wk.keys.reserve(8 * (size_t)std::max<int64_t>(4 * (int64_t)nclauses, 1 << 14)));
-    SATMI_TRY(wk.state.reserve(sizeof(ResState)));
-    SATMI_TRY(wk.passnew.reserve(8 * (size_t)PCAP));
-    SATMI_TRY(wk.stripes.reserve(8 * 2 * RES_STRIPES));
+    SATMI_TRY(wk.state.reserve(SOFF + 8 * (size_t)PCAP));
+    SATMI_TRY(wk.stripes.reserve(8 * RES_STRIPE_ALLOC));
+    SATMI_TRY(wk.pstate.reserve(SOFF + 8 * (size_t)PCAP, hipHostMallocCoherent));
     int64_t key_cap = (int64_t)(wk.keys.cap / 8);
     // stripe regions: twice the key room (the stripes fill unevenly)
     SATMI_TRY(wk.stage.reserve(8 * 2 * (size_t)key_cap));
@@ -912,11 +990,26 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     };
     uint64_t tslots = slots_for(key_cap);
     SATMI_TRY(wk.table.reserve(8 * tslots));
-    ResState &st = *wk.pst;   // the host's copy, refreshed after each batch of passes
+    // the clean slate of the next call (the whole table emptied); cond: only
+    // if the batch just copied out ended the saturation
+    const auto reset = [&](int cond) -> int {
+        const uint64_t all = wk.table.cap / 8;
+        hipLaunchKernelGGL(res_reset_kernel, dim3((unsigned)std::min<uint64_t>(1024, (all + 255) / 256)), dim3(256), 0,
+                           s, wk.table.as<uint64_t>(), all, wk.state.as<ResState>(),
+                           wk.stripes.as<unsigned long long>(), slot_base, cond);
+        SATMI_HIP(hipGetLastError());
+        return SATMI_OK;
+    };
+    // a workspace whose buffers moved since its last reset (or its first call)
+    const ResWork::Clean now{wk.table.p, wk.state.p, wk.stripes.p, slot_base};
+    if (!(wk.clean == now)) SATMI_TRY(reset(0));
+    wk.clean = ResWork::Clean{};   // dirty from here until the reset this call enqueues
+    ResState &st = *(ResState *)wk.pstate.p;   // the host's copy, refreshed after each batch of passes
+    const int64_t *pst_counts = (const int64_t *)(wk.pstate.p + SOFF);
     st = ResState{};
     st.ncl = nclauses;
     st.result = -1;
-    const auto seed = [&](int64_t nkeys) -> int {   // a fresh table holding keys [0, nkeys)
+    const auto seed = [&](int64_t nkeys) -> int {   // a fresh table holding keys [0, nkeys) (regrowth)
         SATMI_HIP(hipMemsetAsync(wk.table.p, 0xFF, 8 * tslots, s));   // HT_EMPTY
         if (nkeys > 0)
             hipLaunchKernelGGL(res_seed_kernel, dim3(grid_for(nkeys)), dim3(256), 0, s, wk.table.as<uint64_t>(),
@@ -925,18 +1018,12 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         SATMI_HIP(hipGetLastError());
         return SATMI_OK;
     };
-    // the state and the stripes set on the device (no copies from the host),
-    // then the keys packed; the deadline is measured from the pack kernel's
-    // start (t0 written by it; no clauses: no pairs, the deadline is never read)
-    const auto prologue = [&]() -> int {
-        hipLaunchKernelGGL(res_init_kernel, dim3(1), dim3(2 * RES_STRIPES), 0, s, wk.state.as<ResState>(),
-                           (int64_t)nclauses, wk.stripes.as<unsigned long long>(), slot_base);
-        if (nclauses > 0)
-            hipLaunchKernelGGL(res_pack_kernel, dim3(grid_for(nclauses)), dim3(256), 0, s,
-                               wk.clauses.as<uint64_t>(), (int64_t)nclauses, wk.keys.as<uint64_t>(),
-                               wk.state.as<ResState>());
-        return seed(nclauses);
-    };
+    // keys, table seed, clause count and the deadline's start (t0): one launch
+    hipLaunchKernelGGL(res_prologue_kernel, dim3(grid_for(std::max(nclauses, 1))), dim3(256), 0, s, nclauses,
+                       (const int32_t *)up, (const int32_t *)(up + o_lits), (const int32_t *)(up + o_map),
+                       wk.keys.as<uint64_t>(), wk.table.as<uint64_t>(), tslots / RES_BUCKET - 1,
+                       wk.state.as<ResState>());
+    SATMI_HIP(hipGetLastError());
     double hz = 1e8;
     (void)satmi_wallclock_hz(&hz);
     ResArgs A;
@@ -947,7 +1034,7 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         A.key_cap = key_cap;
         A.table = wk.table.as<uint64_t>();
         A.tmask = tslots / RES_BUCKET - 1;   // bucket mask
-        A.pass_new = wk.passnew.as<int64_t>();
+        A.pass_new = (int64_t *)(wk.state.as<unsigned char>() + SOFF);
         A.pass_cap = PCAP;
         A.max_passes = max_passes;
         A.clause_limit = clause_limit;
@@ -963,14 +1050,39 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     int64_t rec_clauses = 0, rec_lits = 0;
     std::vector<uint64_t> hkeys;
     const dim3 pass_grid(256, 32);   // j-tiles x i-tiles, grid-stride
-    const auto passes = [&](int batch) -> int {   // a batch of passes, then the state back
+    // A batch of passes, then the state and counts back into pinned memory
+    // with a flag the host spins on, then the next call's reset if the batch
+    // ended the saturation (S->done -- set by an overflow too, whose regrowth
+    // re-uploads the state and re-seeds the table)
+    volatile uint32_t *flag = (volatile uint32_t *)(wk.pin + 7);
+    const auto passes = [&](int batch) -> int {
         for (int b = 0; b < batch; ++b) {
             hipLaunchKernelGGL(res_pass_packed_kernel, pass_grid, dim3(256), 0, s, A);
-            hipLaunchKernelGGL(res_gather_kernel, dim3(8, RES_STRIPES), dim3(256), 0, s, A);
-            hipLaunchKernelGGL(res_finish_pass_kernel, dim3(1), dim3(RES_STRIPES), 0, s, A);
+            hipLaunchKernelGGL(res_gather_kernel, dim3(2, RES_STRIPES), dim3(256), 0, s, A);
         }
+        const int64_t ncopy = h_pass_new ? std::min<int64_t>(PCAP, st.passes + batch) : 0;
+        hipLaunchKernelGGL(res_copyout_kernel, dim3(1), dim3(64), 0, s, wk.state.as<unsigned char>(),
+                           (uint32_t)(SOFF + 8 * (size_t)ncopy), wk.pstate.p, (uint32_t *)flag,
+                           wk.stripes.as<unsigned long long>());
         SATMI_HIP(hipGetLastError());
-        SATMI_HIP(hipMemcpyAsync(wk.pst, wk.state.p, sizeof(ResState), hipMemcpyDeviceToHost, s));
+        return reset(1);
+    };
+    // the batch's copy-out: spin on its flag (a stream wait sleeps ~20 us past
+    // the end of short work), then a stream wait if it takes longer than 2 ms
+    // (a long pass, or a fault: the wait reports it)
+    const auto wait_batch = [&]() -> int {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (*flag == 0u) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                SATMI_HIP(hipStreamSynchronize(s));
+                if (*flag == 0u) {
+                    set_error("satmi_resolution_host: a batch ended without its state");
+                    return SATMI_ERR_HIP;
+                }
+                break;
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
         return SATMI_OK;
     };
     bool first = true;
@@ -979,18 +1091,20 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         const int64_t left = max_passes > 0 ? max_passes - st.passes : 4;
         const int batch = record ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(left, 16));
         const int64_t ncl_before = st.ncl;
-        if (first) {   // the prologue and the first batch: replayed from the graph when they repeat
+        *flag = 0u;
+        std::atomic_thread_fence(std::memory_order_release);
+        if (first) {   // the first batch: replayed from the graph when it repeats
             first = false;
             ResGraph &G = wk.graph;
-            const bool same = G.ncl == nclauses && G.clauses == wk.clauses.p && G.tslots == tslots &&
-                              G.batch == batch && std::memcmp(&G.args, &A, sizeof(ResArgs)) == 0;
+            const void *down = h_pass_new ? (const void *)wk.pstate.p : nullptr;
+            const bool same = G.ncl == nclauses && G.tslots == tslots && G.batch == batch && G.down == down &&
+                              G.pstate == wk.pstate.p && std::memcmp(&G.args, &A, sizeof(ResArgs)) == 0;
             if (same && G.exec) {
                 SATMI_HIP(hipGraphLaunch(G.exec, s));
             } else if (same) {
                 hipGraph_t graph = nullptr;
                 SATMI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-                int rc = prologue();
-                if (rc == SATMI_OK) rc = passes(batch);
+                const int rc = passes(batch);
                 const hipError_t ec = hipStreamEndCapture(s, &graph);
                 if (rc != SATMI_OK || ec != hipSuccess) {
                     if (graph) (void)hipGraphDestroy(graph);
@@ -1006,16 +1120,16 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
                 G.reset();
                 G.args = A;
                 G.ncl = nclauses;
-                G.clauses = wk.clauses.p;
                 G.tslots = tslots;
                 G.batch = batch;
-                SATMI_TRY(prologue());
+                G.down = down;
+                G.pstate = wk.pstate.p;
                 SATMI_TRY(passes(batch));
             }
         } else {
             SATMI_TRY(passes(batch));
         }
-        SATMI_HIP(hipStreamSynchronize(s));
+        SATMI_TRY(wait_batch());
         if (st.overflow) {   // grow the key buffer and / or the table, re-seed, run the pass again
             if (time_limit_s > 0 &&
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t_call).count() >= time_limit_s)
@@ -1041,7 +1155,7 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
             st.empty = 0;
             st.timeout = 0;
             st.count = 0;
-            SATMI_HIP(hipMemcpyAsync(wk.state.p, wk.pst, sizeof(ResState), hipMemcpyHostToDevice, s));
+            SATMI_HIP(hipMemcpyAsync(wk.state.p, wk.pstate.p, sizeof(ResState), hipMemcpyHostToDevice, s));
             SATMI_TRY(seed(st.ncl));   // (after the state: a seed overflow flag must survive)
             continue;
         }
@@ -1056,13 +1170,9 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
         }
         if (st.done) break;
     }
+    // the counts came back with the last batch's state (the stream has drained)
     const int np = (int)std::min<int64_t>(st.passes, std::min(pass_cap, PCAP));
-    if (h_pass_new && np > 0) {   // through pinned memory (a copy into pageable memory is staged)
-        SATMI_TRY(wk.down_h.reserve(8 * (size_t)np));
-        SATMI_HIP(hipMemcpyAsync(wk.down_h.p, wk.passnew.p, 8 * (size_t)np, hipMemcpyDeviceToHost, s));
-    }
-    SATMI_HIP(hipStreamSynchronize(s));
-    if (h_pass_new && np > 0) std::memcpy(h_pass_new, wk.down_h.p, 8 * (size_t)np);
+    if (h_pass_new && np > 0) std::memcpy(h_pass_new, pst_counts, 8 * (size_t)np);
     *h_result = st.result;
     *h_passes = (int32_t)st.passes;
     g_stats.pairs = st.pairs;
@@ -1070,6 +1180,9 @@ int resolution_packed(ResWork &wk, int nclauses, int64_t max_passes, int64_t cla
     g_stats.pair_ms = (double)st.pass_ticks / hz * 1e3;   // device clock, pass kernels only
     g_stats.claim_ms = 0.0;   // fused into the pass kernel
     g_stats.shader_hz = st.clk_ticks ? (double)st.clk_cyc / (double)st.clk_ticks * hz : 0.0;
+    // the last batch ended the saturation (S->done), so its reset is queued:
+    // it runs while this result goes back to the caller
+    wk.clean = now;
     return SATMI_OK;
 }
 
@@ -1180,14 +1293,17 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
         if (L) std::memcpy(wk->up_h.p + o_lits, h_lits, 4 * (size_t)L);
         std::memcpy(wk->up_h.p + o_map, var2dense.data(), 4 * (size_t)(maxvar + 1));
         SATMI_HIP(hipMemcpyAsync(wk->up.p, wk->up_h.p, up_bytes, hipMemcpyHostToDevice, s));
-        const unsigned char *up = (const unsigned char *)wk->up.p;
-        hipLaunchKernelGGL(encode_keys_kernel, dim3(grid_for(nclauses)), dim3(PRIM_BLOCK), 0, s, nclauses,
-                           (const int32_t *)up, (const int32_t *)(up + o_lits), (const int32_t *)(up + o_map), W,
-                           clauses.as<uint64_t>());
-        SATMI_HIP(hipGetLastError());
+        if (!packed) {   // (the packed path encodes its keys in its prologue launch)
+            const unsigned char *up = (const unsigned char *)wk->up.p;
+            hipLaunchKernelGGL(encode_keys_kernel, dim3(grid_for(nclauses)), dim3(PRIM_BLOCK), 0, s, nclauses,
+                               (const int32_t *)up, (const int32_t *)(up + o_lits), (const int32_t *)(up + o_map), W,
+                               clauses.as<uint64_t>());
+            SATMI_HIP(hipGetLastError());
+        }
     }
     if (packed) {
-        const int rc = resolution_packed(*wk, nclauses, max_passes, clause_limit, time_limit_s, slot_base, V,
+        const int rc = resolution_packed(*wk, nclauses, (const unsigned char *)wk->up.p, o_lits, o_map, max_passes,
+                                         clause_limit, time_limit_s, slot_base, V,
                                          dense2var, h_result, h_passes, h_pass_new, pass_cap, h_rec_lits,
                                          rec_lit_cap, h_rec_clause_off, rec_clause_cap, h_rec_pass_off, rec_pass_cap);
         if (rc == SATMI_OK) lease.ok = true;

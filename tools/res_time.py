@@ -11,6 +11,9 @@ import sys
 import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'sat-mpi-stana-andrei_amd'))
+if "--torch" in sys.argv:   # as bench.py: torch (and its HIP runtime setup) loaded first
+    import torch  # noqa: F401,E402
+    torch.cuda.set_device(0)
 import numpy as np  # noqa: E402
 from satmi import _capi, cnf  # noqa: E402
 from satmi.resolution import _csr, _p, last_stats, resolve  # noqa: E402
@@ -34,7 +37,7 @@ for _ in range(50):
     L.satmi_resolution_host(len(f), _p(off), _p(lits), 4, 0, 0.0, ctypes.byref(res), ctypes.byref(passes),
                             _p(pn, ctypes.c_int64), 4, None, 0, None, 0, None, 0)
     tc.append(time.perf_counter() - t)
-print(json.dumps({"lib": sys.argv[1] if len(sys.argv) > 1 else "", "median_ms": float(np.median(ts)) * 1e3,
+print(json.dumps({"lib": " ".join(sys.argv[1:]), "median_ms": float(np.median(ts)) * 1e3,
                   "min_ms": min(ts) * 1e3, "c_call_median_ms": float(np.median(tc)) * 1e3,
                   "pair_ms": st["pair_ms"], "shader_clock_hz": st.get("shader_clock_hz"), "pass_new": r["pass_new"],
                   "derived_per_s": sum(r["pass_new"]) / float(np.median(ts))}))
