@@ -808,12 +808,21 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
     }
 }
 
+// IN_LDS: [val, pool) of the layout and the learned-literal scratch live in
+// the wave's LDS (A.lay.lds_bytes > 0).  A compile-time choice, so that every
+// access is a ds_* or a global_* instruction: a pointer picked at run time
+// between the two is generic, and flat instructions (both wait counters, no
+// LDS fast path) were every access of the kernel.
+template <bool IN_LDS>
 __global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char cdcl_lds[];
     unsigned char *base = A.arena + (size_t)blockIdx.x * (size_t)A.lay.bytes;
     // [val, pool) of the layout, relocated into LDS when it fits
     const auto small = [&](uint64_t off) -> unsigned char * {
-        return A.lay.lds_bytes ? cdcl_lds + (off - A.lay.val) : base + off;
+        if constexpr (IN_LDS)
+            return cdcl_lds + (off - A.lay.val);
+        else
+            return base + off;
     };
     St S;
     S.coff = (int64_t *)(base + A.lay.coff);
@@ -835,7 +844,10 @@ __global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
     __shared__ uint64_t clk_s[16];
     S.clk = clk_s;
 #endif
-    S.scratch = A.lay.lds_bytes ? (int32_t *)(cdcl_lds + A.lay.lds_scratch) : (int32_t *)(base + A.lay.scratch);
+    if constexpr (IN_LDS)
+        S.scratch = (int32_t *)(cdcl_lds + A.lay.lds_scratch);
+    else
+        S.scratch = (int32_t *)(base + A.lay.scratch);
     span_begin(A.work_counter);
     uint64_t busy = 0;   // this wave's ticks spent solving (the rest of its residency is the launch's tail)
     for (;;) {
@@ -1079,7 +1091,10 @@ extern "C" int satmi_cdcl_batch_host(int num_instances, const int32_t *h_inst_cl
         A.arena = d + o_arena;
         A.lay = lay;
         A.work_counter = (uint32_t *)(d + o_wc);
-        hipLaunchKernelGGL(cdcl_kernel, dim3(grid), dim3(64), lay.lds_bytes, s, A);
+        if (lay.lds_bytes)
+            hipLaunchKernelGGL(cdcl_kernel<true>, dim3(grid), dim3(64), lay.lds_bytes, s, A);
+        else
+            hipLaunchKernelGGL(cdcl_kernel<false>, dim3(grid), dim3(64), 0, s, A);
         hipError_t e = hipGetLastError();
         auto d2h = [&](void *dst, size_t off, size_t bytes) {
             if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, d + off, bytes, hipMemcpyDeviceToHost, s);

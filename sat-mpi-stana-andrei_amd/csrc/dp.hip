@@ -72,6 +72,18 @@ enum : int32_t { OVF_PAIRS = 1, OVF_NCL = 2, OVF_ARENA = 4, OVF_XS = 8 };
 
 constexpr uint64_t DP_EMPTY = ~0ull;
 constexpr int DP_STRIPES = 64;
+#ifndef DP_GRID_PAIRS   // grid caps of the step's kernels (grid-stride: a cap only bounds the dispatch)
+#define DP_GRID_PAIRS 1024
+#endif
+#ifndef DP_GRID_TEST
+#define DP_GRID_TEST 2048
+#endif
+#ifndef DP_GRID_ASM
+#define DP_GRID_ASM 2048
+#endif
+#ifndef DP_GRID_GATHER
+#define DP_GRID_GATHER 64
+#endif
 constexpr int DP_LAUNCHES_PER_STEP = 9;   // pop_split, pairs, hash, gather, remtest, survlist, survtest, kept, assemble
 
 // The solve's state, on the device.  Host writes it once per solve (and on a
@@ -1303,14 +1315,14 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     };
     // one elimination step: DP_LAUNCHES_PER_STEP launches, sizes on the device
     const auto enqueue_step = [&](const DpArgs &a) -> int {
-        const int gp = (int)std::min<int64_t>(1024, (a.pair_cap + 255) / 256);
-        const int gc = (int)std::min<int64_t>(2048, (a.ncl_cap + ASM_WAVES - 1) / ASM_WAVES);
+        const int gp = (int)std::min<int64_t>(DP_GRID_PAIRS, (a.pair_cap + 255) / 256);
+        const int gc = (int)std::min<int64_t>(DP_GRID_ASM, (a.ncl_cap + ASM_WAVES - 1) / ASM_WAVES);
         hipLaunchKernelGGL(dp_pop_split_kernel, dim3(1), dim3(POP_THREADS), 0, s, a);
         hipLaunchKernelGGL(dp_pairs_kernel, dim3(gp), dim3(256), 0, s, a);
         hipLaunchKernelGGL(dp_hash_kernel, dim3(gp), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(dp_gather_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(64, a.pair_cap / (DP_STRIPES * 256))), DP_STRIPES),
+        hipLaunchKernelGGL(dp_gather_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(DP_GRID_GATHER, a.pair_cap / (DP_STRIPES * 256))), DP_STRIPES),
                            dim3(256), 0, s, a);
-        const dim3 gt((unsigned)std::min<int64_t>(2048, std::max<int64_t>(64, a.pair_cap / 256)));
+        const dim3 gt((unsigned)std::min<int64_t>(DP_GRID_TEST, std::max<int64_t>(64, a.pair_cap / 256)));
         switch (a.K) {
             case 2: hipLaunchKernelGGL(dp_remtest_kernel<2>, gt, dim3(TEST_TILE), 0, s, a); break;
             case 4: hipLaunchKernelGGL(dp_remtest_kernel<4>, gt, dim3(TEST_TILE), 0, s, a); break;
