@@ -676,6 +676,7 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
             int32_t cnt = analyze_conflict(S, conflict, A.lay.lcap, &bt);   // the whole wave
             cnt = __builtin_amdgcn_readfirstlane(cnt);
             bt = __builtin_amdgcn_readfirstlane(bt);
+            CDCL_CLK(S, 13);
             if (cnt > 0) {   // learn_clause (REF.py:347-357), wave-uniform
                 if (q.nf + 1 > A.lay.clause_cap || q.nlits + cnt > A.lay.lit_cap) {
                     q.full = true;
@@ -713,6 +714,7 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
                     wave_sync();
                 }
             }
+            CDCL_CLK(S, 14);
             if (cnt == -2) q.full = true;   // scratch list bound (see analyze_conflict)
             else if (cnt < 0) {
                 status = CD_ERROR;
@@ -802,7 +804,9 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
         for (int i = 0; i < 4; ++i) st[4 + i] = (int64_t)S.clk[i];
         for (int i = 0; i < 3; ++i) st[1 + i] = (int64_t)S.clk[4 + i];   // moves, entries, lists
         // (over the model row) clocks in watch adds, in resizes, resizes, entries moved by them, adds
-        for (int i = 0; i < 5 && i < A.assign_stride; ++i) out[i] = (int32_t)min<uint64_t>(S.clk[8 + i], INT32_MAX);
+        // then clocks in analyze_conflict and in learn_clause (their watch adds included)
+        for (int i = 0; i < 7 && i < A.assign_stride; ++i)
+            out[i] = (int32_t)min<uint64_t>(S.clk[8 + i], INT32_MAX);
 #endif
         A.var_inc[b] = q.var_inc;
     }

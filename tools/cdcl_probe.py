@@ -7,8 +7,9 @@ Diagnostic build only (never the product):
 The phase build overwrites the stats columns (csrc/cdcl.hip solve_one): [1..3]
 = watch moves, snapshot entries, false watch lists visited; [4..7] = shader
 clocks in snapshots, replacement watches, watch-list moves, and everything
-between propagate calls; the model row's first five entries = clocks in watch
-adds, clocks in table resizes, resizes, entries they moved, watch adds.  Printed per iteration over the iteration-capped
+between propagate calls; the model row's first seven entries = clocks in watch
+adds, clocks in table resizes, resizes, entries they moved, watch adds, clocks
+in analyze_conflict, clocks in learn_clause (of the "between" clocks).  Printed per iteration over the iteration-capped
 solves (the launch's tail) and over the rest, plus the launch's wall time.
 """
 import argparse
@@ -52,7 +53,8 @@ def main():
                                        "clk_moves": s[sel, 6].sum() / it, "clk_between": s[sel, 7].sum() / it,
                                        "clk_watch_adds": asg[sel, 0].sum() / it, "clk_resizes": asg[sel, 1].sum() / it,
                                        "resizes": asg[sel, 2].sum() / it, "resize_entries": asg[sel, 3].sum() / it,
-                                       "watch_adds": asg[sel, 4].sum() / it}}
+                                       "watch_adds": asg[sel, 4].sum() / it,
+                                       "clk_analyze": asg[sel, 5].sum() / it, "clk_learn": asg[sel, 6].sum() / it}}
     print(json.dumps(out))
 
 
