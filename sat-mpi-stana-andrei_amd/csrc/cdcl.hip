@@ -46,7 +46,7 @@ namespace {
 
 constexpr int32_t WS_EMPTY = 0, WS_DUMMY = INT32_MIN;
 constexpr int WS_MINSIZE = 8, WS_PROBES = 9, WS_PERTURB = 5;
-constexpr int64_t ANTE_ABSENT = -2;
+constexpr int32_t ANTE_ABSENT = -2;
 constexpr double VAR_DECAY = 0.95;
 
 enum { CD_FALSE = 0, CD_TRUE = 1, CD_LIMIT = -1, CD_ERROR = -2, CD_FULL = -3 };
@@ -80,16 +80,16 @@ struct CdclArgs {
 };
 
 struct St {   // views into one wave's arena
-    int64_t *coff;
+    int32_t *coff;   // (32-bit offsets and indices: make_cdcl_layout bounds the arena below 2^31 entries)
     int32_t *lits;
     int8_t *val;
     int64_t *ord;
     int32_t *lev;
-    int64_t *ante;
+    int32_t *ante;
     double *act;
     uint64_t *appears;
     int32_t *klit, *kidx;
-    int64_t *woff;
+    int32_t *woff;
     int32_t *wmask, *wfill, *wused;
     int32_t *pool, *scratch;
 #ifdef SATMI_CDCL_PHASES
@@ -232,7 +232,7 @@ __device__ void ws_resize(const CdclArgs &A, const St &S, Seq &q, int k, int64_t
             if (ot[i] != WS_EMPTY && ot[i] != WS_DUMMY) ws_insert_clean(nt, nmask, ot[i]);
     }
     if (ln == 0) {
-        S.woff[k] = off;
+        S.woff[k] = (int32_t)off;
         S.wmask[k] = (int32_t)nmask;
         S.wfill[k] = S.wused[k];
     }
@@ -302,7 +302,7 @@ __device__ int key_of(const CdclArgs &A, const St &S, Seq &q, int lit) {
     if (ln == 0) {
         S.klit[k] = lit;
         S.kidx[c] = k + 1;
-        S.woff[k] = off;
+        S.woff[k] = (int32_t)off;
         S.wmask[k] = WS_MINSIZE - 1;
         S.wfill[k] = S.wused[k] = 0;
     }
@@ -387,7 +387,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                 }
             }
             int32_t x[4], lit[4];
-            int64_t at[4];
+            int at[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {   // up to four table reads in flight
                 const int g = g0 + 64 * u + ln;
@@ -398,7 +398,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                 x[u] = in ? S.pool[at[u]] : WS_EMPTY;
             }
             bool act[4];
-            int64_t jb[4], je[4];
+            int jb[4], je[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 act[u] = x[u] != WS_EMPTY && x[u] != WS_DUMMY;
@@ -425,7 +425,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                     r[u] = (r[u] == 0 && ot != lit[u] && (v < 0 || (ot > 0) == (v != 0))) ? ot : r[u];
                 }
                 if (act[u] && r[u] == 0) {   // longer clauses: the rest one literal at a time
-                    for (int64_t j = jb[u] + CDCL_LITS_AHEAD; j < je[u]; ++j) {
+                    for (int j = jb[u] + CDCL_LITS_AHEAD; j < je[u]; ++j) {
                         const int ot = S.lits[j];
                         if (ot == lit[u]) continue;
                         const int8_t v = S.val[iabs(ot)];
@@ -504,7 +504,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
 __device__ int analyze_conflict(const St &S, int64_t conflict, int32_t cap, int32_t *bt) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
-    const int64_t jb = S.coff[conflict], je = S.coff[conflict + 1];
+    const int jb = S.coff[conflict], je = S.coff[conflict + 1];
     if (je - jb > cap) return -2;
     int32_t *L = S.scratch, *N = S.scratch + cap;
     int n = (int)(je - jb);
@@ -541,13 +541,13 @@ __device__ int analyze_conflict(const St &S, int64_t conflict, int32_t cap, int3
                 break;
             }
         }
-        const int64_t a = S.ante[iabs(last)];
+        const int a = S.ante[iabs(last)];
         if (a < 0) {   // None or -1
             *bt = sc;
             return n;
         }
         // resolve with the antecedent (REF.py:331-342): new list at scratch + cap
-        const int64_t ab = S.coff[a], ae = S.coff[a + 1];
+        const int ab = S.coff[a], ae = S.coff[a + 1];
         const int alen = (int)(ae - ab);
         int m = 0;
         for (int i0 = 0; i0 < n; i0 += 64) {   // kept literals, in order (m <= n <= cap)
@@ -634,7 +634,7 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
     q.full = false;
     // setup_watch_list (REF.py:233-244), wave-uniform
     for (int64_t i = 0; i < m && !q.full; ++i) {
-        const int64_t jb = S.coff[i], len = S.coff[i + 1] - jb;
+        const int jb = S.coff[i], len = S.coff[i + 1] - jb;
         if (len > 1) {
             watch_add(A, S, q, S.lits[jb], i);
             watch_add(A, S, q, S.lits[jb + 1], i);
@@ -645,7 +645,7 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
                     S.val[v] = x > 0;
                     S.ord[v] = q.next_ord;
                     S.lev[v] = 0;
-                    S.ante[v] = i;
+                    S.ante[v] = (int32_t)i;
                 }
                 ++q.next_ord;
             }
@@ -684,7 +684,7 @@ __device__ void solve_one(const CdclArgs &A, const St &S, int b) {
                     const int64_t idx = q.nf;
                     for (int i = ln; i < cnt; i += 64) S.lits[q.nlits + i] = S.scratch[i];
                     q.nlits += cnt;
-                    if (ln == 0) S.coff[idx + 1] = q.nlits;
+                    if (ln == 0) S.coff[idx + 1] = (int32_t)q.nlits;
                     q.nf = idx + 1;
                     if (cnt > 1) {
                         watch_add(A, S, q, S.scratch[0], idx);
@@ -829,17 +829,17 @@ __global__ void __launch_bounds__(64) cdcl_kernel(CdclArgs A) {
             return base + off;
     };
     St S;
-    S.coff = (int64_t *)(base + A.lay.coff);
+    S.coff = (int32_t *)(base + A.lay.coff);
     S.lits = (int32_t *)(base + A.lay.lits);
     S.val = (int8_t *)small(A.lay.val);
     S.ord = (int64_t *)small(A.lay.ord);
     S.lev = (int32_t *)small(A.lay.lev);
-    S.ante = (int64_t *)small(A.lay.ante);
+    S.ante = (int32_t *)small(A.lay.ante);
     S.act = (double *)small(A.lay.act);
     S.appears = (uint64_t *)small(A.lay.appears);
     S.klit = (int32_t *)small(A.lay.klit);
     S.kidx = (int32_t *)small(A.lay.kidx);
-    S.woff = (int64_t *)small(A.lay.woff);
+    S.woff = (int32_t *)small(A.lay.woff);
     S.wmask = (int32_t *)small(A.lay.wmask);
     S.wfill = (int32_t *)small(A.lay.wfill);
     S.wused = (int32_t *)small(A.lay.wused);
@@ -881,17 +881,17 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     const int64_t P = 16 * 2 * C + (int64_t)WS_MINSIZE * K;
     auto a = [](uint64_t x) { return (x + 255u) & ~(uint64_t)255u; };
     uint64_t o = 0;
-    L->coff = o;    o = a(o + 8 * (uint64_t)(C + 1));
+    L->coff = o;    o = a(o + 4 * (uint64_t)(C + 1));
     L->lits = o;    o = a(o + 4 * (uint64_t)Lc);
     L->val = o;     o = a(o + (uint64_t)N);
     L->ord = o;     o = a(o + 8 * (uint64_t)N);
     L->lev = o;     o = a(o + 4 * (uint64_t)N);
-    L->ante = o;    o = a(o + 8 * (uint64_t)N);
+    L->ante = o;    o = a(o + 4 * (uint64_t)N);
     L->act = o;     o = a(o + 8 * (uint64_t)N);
     L->appears = o; o = a(o + 8 * (uint64_t)(N / 64 + 1));
     L->klit = o;    o = a(o + 4 * (uint64_t)K);
     L->kidx = o;    o = a(o + 4 * (uint64_t)K);
-    L->woff = o;    o = a(o + 8 * (uint64_t)K);
+    L->woff = o;    o = a(o + 4 * (uint64_t)K);
     L->wmask = o;   o = a(o + 4 * (uint64_t)K);
     L->wfill = o;   o = a(o + 4 * (uint64_t)K);
     L->wused = o;   o = a(o + 4 * (uint64_t)K);
@@ -906,7 +906,8 @@ bool make_cdcl_layout(int max_vars, int64_t max_clauses, int64_t max_lits, int m
     L->lit_cap = Lc;
     L->pool_cap = P;
     L->ncap = max_vars;
-    return max_vars >= 0 && max_vars < (1 << 29);
+    // clause offsets, literal indices and table offsets are 32-bit in the kernel
+    return max_vars >= 0 && max_vars < (1 << 29) && C < INT32_MAX && Lc < INT32_MAX && P < INT32_MAX;
 }
 
 // Device memory of satmi_cdcl_batch_host, kept between calls (grow-only): the
