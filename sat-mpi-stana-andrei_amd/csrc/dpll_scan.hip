@@ -333,7 +333,7 @@ constexpr int FAST_BATCH = 16;
 
 template <int K, typename C>
 __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t ep, uint32_t bep, int *empty_at,
-                         PhaseClock &ph) {
+                         int *pre, PhaseClock &ph) {
     using W = typename Pack<K>::W;
     const int ln = lane_id();
     ph.count(0);
@@ -386,23 +386,34 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
             if (__builtin_expect(nun <= FAST_UNITS, 1)) {
                 ph.count(3);
                 // a clause reached from two batch literals is one snapshot entry
-                bool dup = false;
                 uint64_t dm = um;
                 int rank = 0;
-                if (nun == 2) {   // lanes u0 < u1 (one unit: snapshot index 0)
+                // The next batch is assigned right here -- REF.py:146-155 on a
+                // snapshot of at most two entries: both are assigned unless they
+                // name one variable (the first wins) -- so the next round skips
+                // the snapshot's write-back and its stamp pass.
+                const uint32_t code = unit_code<K>(w, x);
+                bool keep = unit;
+                int nkeep = nun;
+                if (nun == 2) {   // lanes u0 < u1
                     const int u0 = __builtin_ctzll(um), u1 = 63 - __builtin_clzll(um);
                     const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)c, u0);
                     const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)c, u1);
-                    dup = (ln == u1) & (c0 == c1);
+                    const uint32_t v0 = (uint32_t)__builtin_amdgcn_readlane((int)code, u0) >> 1;
+                    const uint32_t v1 = (uint32_t)__builtin_amdgcn_readlane((int)code, u1) >> 1;
                     dm = c0 == c1 ? 1ull << u0 : um;   // a duplicate keeps lane u0 only
                     rank = ln == u0 ? (c1 < c0 ? 1 : 0) : (c0 < c1 ? 1 : 0);
+                    const bool one = (c0 == c1) | (v0 == v1);   // one entry is assigned: the first in clause order
+                    keep = unit & (!one | (rank == 0));
+                    nkeep = one ? 1 : 2;
                 }
-                if (unit && !dup) {
-                    const uint32_t code = unit_code<K>(w, x);
-                    S.snap[rank] = (C)code;
-                    ts_stamp(S, code >> 1, stamp(ep, (uint32_t)rank));
+                if (keep) {
+                    S.trail[tl + rank] = (C)code;
+                    lv_assign(S.lv, code);
+                    S.ts[code >> 1] = stamp(ep, (uint32_t)rank);
                 }
                 wave_sync();
+                *pre = nkeep;
                 return __popcll(dm);
             }
             // more units than the register ranking takes: the touched clauses
@@ -571,10 +582,14 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
     // kept) is not a propagation in REF.py's counters: taken off once here
     props -= dec ? 1u : 0u;
     ph.count(14);
+    int pre = -1;   // >= 0: the unit scan assigned the next batch itself (this many entries)
     while (nu > 0) {
         ++rounds;
         rs = tl;
         const uint32_t bep = ep;   // the batch's epoch
+        if (pre >= 0) {
+            tl += pre;
+        } else {
         int k0 = 0;
         do {   // nu > 0: at least one step
             ph.count(15);
@@ -597,9 +612,11 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             k0 += 64;
         } while (k0 < nu);
         wave_sync();
+        }
         ph.mark(PH_ASSIGN);
         const int nassign = tl - rs;
-        const int nu_next = INC ? inc_units<K>(S, (mpad + 31) >> 5, rs, tl, ++ep, bep, &e, ph)
+        pre = -1;
+        const int nu_next = INC ? inc_units<K>(S, (mpad + 31) >> 5, rs, tl, ++ep, bep, &e, &pre, ph)
                                 : scan_units<K>(S, mpad, ++ep, bep, &e);
         ph.mark(PH_UNITS);
         if (__builtin_expect(e != INT_MAX, 0)) break;
