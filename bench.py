@@ -69,11 +69,14 @@ FIX_NCAP, FIX_MCAP = 127, 448  # dpll_fixed_kernel's shape class (csrc/dpll_scan
 WORKLOADS = {
     "3sat-n100": (262144, 100, 4.26, 3, 0, "configs[2]"),
     "3sat-n50": (4096, 50, 4.26, 3, 0, "configs[1]"),
-    "uf250": (6144, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,072 resident waves
-    "5sat-n200": (1536, 200, 21.117, 5, 20000, "configs[4]"),  # 2 x the 768 resident waves
+    "uf250": (6656, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,328 resident waves (13 / CU)
+    "5sat-n200": (2048, 200, 21.117, 5, 20000, "configs[4]"),  # 2 x the 1,024 resident waves (4 / CU)
 }
 # configs[3] presets: (holes, resolution passes) -- one formula per step, host-array C ABI
 SATURATION = {"php-dp": (5, 0), "php-res": (3, 4)}
+# configs[3]'s "small random UNSAT sets": (solver, formulas per step, n, m, seed) --
+# random 3-SAT past the threshold, each formula saturated / eliminated to the end
+RANDSETS = {"rand-res": ("res", 16, 7, 49, 7001), "rand-dp": ("dp", 16, 16, 96, 7002)}
 # CDCL preset: (formulas per step, clauses, max literals per clause, variables, max_iter, seed)
 CDCL = {"cdcl": (32768, 80, 3, 15, 10000, 1234)}
 
@@ -84,6 +87,8 @@ LEGS = [
     ("configs[3] php-dp", "php-dp", ["--steps", "40", "--warmup", "3"]),
     ("configs[3] php-dp 8 threads", "php-dp", ["--steps", "10", "--warmup", "2", "--threads", "8"]),
     ("configs[3] php-res", "php-res", ["--steps", "20", "--warmup", "2"]),
+    ("configs[3] rand-res", "rand-res", ["--steps", "3", "--warmup", "1"]),
+    ("configs[3] rand-dp 8 threads", "rand-dp", ["--steps", "3", "--warmup", "1", "--threads", "8"]),
     ("configs[4] uf250", "uf250", ["--steps", "4", "--warmup", "1"]),
     ("configs[4] 5sat-n200", "5sat-n200", ["--steps", "4", "--warmup", "1"]),
     # configs[4] solved to the end (no node limit): 512 uf250-shaped searches per
@@ -100,7 +105,7 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(SATURATION) + sorted(CDCL),
+    p.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(SATURATION) + sorted(RANDSETS) + sorted(CDCL),
                    default="3sat-n100")
     p.add_argument("--total", type=int, default=None, help="instances per step, all ranks")
     p.add_argument("--n", type=int, default=None)
@@ -770,9 +775,91 @@ def run_cdcl(args, world, rank, local):
     return out
 
 
+def run_randset(args, world, rank, local):
+    """configs[3]'s small random UNSAT sets: a step = every formula of a fixed
+    set of random 3-SAT formulas past the threshold saturated by resolution
+    (REF.py:63-95, to the empty clause or no new clause) or eliminated by
+    Davis-Putnam (REF.py:98-130), one satmi call per formula (host arrays in,
+    verdict out); `--threads` T splits the set over T host threads (one HIP
+    stream each).  Each rank solves its own replica of the set."""
+    from satmi.dp import eliminate
+    from satmi.resolution import resolve
+    from concurrent.futures import ThreadPoolExecutor
+    torch.cuda.set_device(local)
+    kind, count, n, m, seed = RANDSETS[args.workload]
+    batch = cnf.uniform_ksat(count, n, m, 3, seed=seed)
+    fs = [batch.instance(b) for b in range(count)]
+    T = max(1, args.threads)
+
+    def part(t):
+        torch.cuda.set_device(local)
+        return [(b, resolve(fs[b]) if kind == "res" else eliminate(fs[b])) for b in range(t, count, T)]
+
+    pool = ThreadPoolExecutor(T) if T > 1 else None
+    run = (lambda: sorted(x for ys in pool.map(part, range(T)) for x in ys)) if pool else (lambda: part(0))   # noqa: E731
+    for _ in range(0 if args.profile_steps else args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    derived = 0
+    last = None
+    for _ in range(args.steps):
+        last = run()
+        derived += sum(sum(r["pass_new"]) for _, r in last) if kind == "res" else 0
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local))
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    if pool:
+        pool.shutdown()
+    results = [r["result"] for _, r in last]
+    desc = (f"{'resolution saturation' if kind == 'res' else 'Davis-Putnam elimination'} of {count} random 3-SAT "
+            f"formulas n={n} m={m} (alpha={m / n:g}) to the end")
+    out = {"metric": METRIC, "value": count * args.steps * world / elapsed, "unit": "formulas/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+           "data": "synthetic: seeded uniform random 3-SAT",
+           "config": {"workload": desc + " (BASELINE configs[3]: small random UNSAT sets); replicas across ranks"
+                                  + (f"; {T} host threads" if T > 1 else ""),
+                      "preset": args.workload, "parallelism": f"replicas x{world}", "concurrent_solves": T},
+           "result": results, "unsat": results.count(0), "roofline": None}
+    if kind == "res":
+        out["derived_clauses_per_s"] = derived * world / elapsed
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        # the oracle on the first formulas (resolution: ~2 s each on one core): verdicts
+        # and per-pass counts / eliminated variables checked against the GPU's
+        nchk = 2 if kind == "res" else count
+        for b, r in last[:nchk]:
+            o = oracle.resolution(fs[b]) if kind == "res" else oracle.dp(fs[b])
+            got = (r["result"], list(r["pass_new"])) if kind == "res" else (r["result"], list(r["vars"]))
+            exp = (o["result"], list(o["pass_new"])) if kind == "res" else (o["result"], list(o["vars"]))
+            if got != exp:
+                raise SystemExit(f"bench: GPU and oracle disagree on {args.workload} formula {b}: {got} vs {exp}")
+        out["oracle_check"] = {"formulas_checked": nchk}
+        pres, cores = cpu_pool(kind + "set", batch.inst_clause_begin, batch.clause_lit_begin, batch.lits,
+                               args.cpu_seconds, 0)
+        cpu = {"value": pres["units_per_s"], "unit": "formulas/s", "cores": cores, "kind": "port",
+               "sample": f"the same {count} formulas by the oracle (oracle/*.c), worker w solving formulas w, "
+                         f"w + {cores}, ... (cycling) on {cores} worker processes (one per host core) for "
+                         f"{pres['seconds']:.1f} s: {pres['units']} formulas"}
+    out["cpu_baseline"] = cpu
+    return out
+
+
 def run_one(args, world, rank, local):
     if args.workload in SATURATION:
         return run_saturation(args, world, rank, local)
+    if args.workload in RANDSETS:
+        return run_randset(args, world, rank, local)
     if args.workload in CDCL:
         return run_cdcl(args, world, rank, local)
     out, host = run_dpll(args, world, rank, local)
@@ -794,7 +881,8 @@ def legs_main(args):
         keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_issue",
                 "cpu_baseline", "result", "passes_or_steps", "instances_per_s", "unit_props_per_s",
                 "capped_fraction", "sat_fraction", "sat", "unsat", "iteration_capped", "iterations_per_s",
-                "verdict_sha", "kernel_ms", "wave_utilisation", "oracle_check", "resident_waves", "branch_split")
+                "verdict_sha", "kernel_ms", "wave_utilisation", "oracle_check", "resident_waves", "branch_split",
+                "derived_clauses_per_s")
         out[name] = {k: r[k] for k in keep if k in r}
         out[name]["leg_wall_s"] = time.perf_counter() - t
     print(json.dumps(out), flush=True)

@@ -15,6 +15,9 @@ memory-mapped by every worker.  Kinds:
     dp    Davis-Putnam (REF.py:98-130) of instance 0, repeated (replicas)
     res   resolution (REF.py:63-95) of instance 0, <param> = passes, repeated;
           the unit is derived clauses
+    resset / dpset  resolution / Davis-Putnam of every instance to the end,
+          worker w solving instances w, w + workers, ... and cycling over the
+          set until the time is up; the unit is formulas
 until `seconds` pass (every worker finishes at least one unit).  Prints one
 JSON line: units and unit-props (dpll) per second over the slowest worker's
 wall time.
@@ -49,6 +52,12 @@ def _solve(kind, f, param):
         return 1, 0
     if kind == "res":
         return sum(oracle.resolution(f, max_passes=param)["pass_new"]), 0
+    if kind == "resset":
+        oracle.resolution(f)
+        return 1, 0
+    if kind == "dpset":
+        oracle.dp(f)
+        return 1, 0
     raise ValueError(kind)
 
 
@@ -60,13 +69,16 @@ def _worker(args):
     t0 = time.perf_counter()
     done = props = 0
     replicas = kind in ("dp", "res")
+    cycle = kind in ("resset", "dpset")
     f0 = _instance(icb, clb, lits, 0) if replicas else None
-    b = w
-    while replicas or b < B:
+    b = w % B
+    while replicas or cycle or b < B:
         u, p = _solve(kind, f0 if replicas else _instance(icb, clb, lits, b), param)
         done += u
         props += p
         b += workers
+        if cycle:
+            b %= B
         if time.perf_counter() - t0 > seconds:
             break
     return done, props, time.perf_counter() - t0

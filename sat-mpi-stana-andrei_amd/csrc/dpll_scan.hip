@@ -134,13 +134,17 @@ struct ScanArgs {
     int64_t *counters;
     int32_t *sol_len, *sol_lits, *root_len, *root_lits;
     uint32_t *work_counter;
-    uint16_t *occ;      // incremental kernel: per-wave occurrence-list scratch (HBM/L2), occ_cap entries each
-    int32_t occ_cap;
+    uint16_t *occ;      // per-wave HBM/L2 scratch, occ_cap entries each: the incremental kernel's
+    int32_t occ_cap;    // occurrence lists [0, occ_lists), then the snapshot entries past snap_lds
     ScanLayout lay;
     // branch splitting (see "Splitting the tail" below); nullptr: off.  Its
     // geometry lives in device memory, not in kernel arguments: the node loop
     // is SGPR-bound, and only this pointer stays live across it.
     struct SplitCfg *split;
+    // (last: the fields above keep their kernel-argument offsets -- the node
+    // loop's SGPR allocation is sensitive to them)
+    int32_t occ_lists;
+    uint32_t snap_lds;   // snapshot entries in LDS (16-bit codes; see snap_put)
 };
 
 // C: the type of a literal code / variable / trail position in the trail,
@@ -158,8 +162,10 @@ struct SLds {
     C *trail;                   // [ncap+1]  assignment order (literal codes) == dict insertion order
     C *fvar;                    // [ncap+1]  decision frames: var | PHASE_BIT once False runs
     C *ftrail;                  // [ncap+1]  trail length before the decision
-    C *snap;                    // scratch:  unit-clause snapshot (propagation)
+    C *snap;                    // scratch:  unit-clause snapshot (propagation), entries [0, scap)
     uint32_t *plist;            // scratch:  pure-literal positions (analysis), aliases snap
+    C *snapg;                   // global:   snapshot entries [scap, m] (16-bit codes only)
+    uint32_t scap;
     // incremental kernel only
     uint16_t *occ_off;          // [2(ncap+1)+1]  start of each literal code's occurrence list in `occ`
     uint2 *bm;                  // [nw]  unit bitmap of the round: .x one bit per clause (32 clauses
@@ -255,6 +261,33 @@ constexpr uint32_t EPOCH_LIMIT = 0xFFFFu - 4096u;   // > rounds of one propagate
 __device__ __forceinline__ uint32_t stamp(uint32_t ep, uint32_t k) { return ((ep << 16) | 0xFFFFu) - k; }   // k <= 0xFFFF
 __device__ __forceinline__ uint32_t stamp_index(uint32_t st) { return 0xFFFFu - (st & 0xFFFFu); }
 
+// Snapshot entry k.  With byte codes (n <= 127) the whole snapshot is in LDS;
+// with 16-bit codes the first `scap` entries are (a few hundred: a round finds
+// tens of units), the rest of a larger snapshot goes to the wave's HBM scratch,
+// so the LDS does not hold m entries that are almost never used (5-SAT n=200:
+// 8.4 KB of 47 KB per wave, the difference between 3 and 4 waves per CU).
+template <int K, typename C>
+__device__ __forceinline__ void snap_put(const SLds<K, C> &S, uint32_t k, uint32_t code) {
+    if constexpr (sizeof(C) == 1) {
+        S.snap[k] = (C)code;
+    } else {
+        if (k < S.scap) S.snap[k] = (C)code;
+        else S.snapg[k - S.scap] = (C)code;
+    }
+}
+template <int K, typename C>
+__device__ __forceinline__ uint32_t snap_get(const SLds<K, C> &S, uint32_t k) {
+    if constexpr (sizeof(C) == 1) return S.snap[k];
+    else return k < S.scap ? (uint32_t)S.snap[k] : (uint32_t)S.snapg[k - S.scap];
+}
+// before a snapshot of nu entries is read back: the HBM part written by other
+// lanes of this wave is complete (the occurrence lists' recipe)
+template <int K, typename C>
+__device__ __forceinline__ void snap_ready(const SLds<K, C> &S, int nu) {
+    if constexpr (sizeof(C) == 2)
+        if ((uint32_t)nu > S.scap) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
 // Scan for unit_propagate: the unit-clause snapshot (REF.py:143), in clause
 // order, into S.snap, each entry's variable stamped with epoch `ep` (the first
 // occurrence of a variable keeps the smallest index: REF.py:149-152's
@@ -288,7 +321,7 @@ __device__ int scan_units(const SLds<K, C> &S, int mpad, uint32_t ep, uint32_t b
         if (unit) {
             const uint32_t k = (uint32_t)nu + (uint32_t)__popcll(mk & lt);
             const uint32_t code = unit_code<K>(S.cls[c], x);   // re-read: keeps U words out of VGPRs
-            S.snap[k] = (C)code;
+            snap_put(S, k, code);
             ts_stamp(S, code >> 1, stamp(ep, k));
         }
         nu += __popcll(mk);
@@ -444,7 +477,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
                 const uint2 pb = S.bm[c >> 5];
                 const uint32_t k = pb.y + (uint32_t)__popc(pb.x & ((1u << (c & 31u)) - 1u));
                 const uint32_t code = unit_code<K>(w, x);
-                S.snap[k] = (C)code;
+                snap_put(S, k, code);
                 ts_stamp(S, code >> 1, stamp(ep, k));
                 // clean bitmap for the next round: only the words units set (a
                 // wave's LDS operations run in order, so every lane of the word
@@ -530,7 +563,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
         if (unit) {
             const uint2 p = S.bm[uc >> 5];
             const uint32_t k = p.y + (uint32_t)__popc(p.x & ((1u << (uc & 31u)) - 1u));
-            S.snap[k] = (C)ucode;
+            snap_put(S, k, ucode);
             ts_stamp(S, ucode >> 1, stamp(ep, k));
         }
     } else {
@@ -546,7 +579,7 @@ __device__ int inc_units(const SLds<K, C> &S, int nw, int rs, int tl, uint32_t e
 #pragma unroll
                 for (int j = 0; j < K; ++j) x[j] = lv_get(S, field<K>(wd, j));
                 const uint32_t code = unit_code<K>(wd, x);
-                S.snap[k] = (C)code;
+                snap_put(S, k, code);
                 ts_stamp(S, code >> 1, stamp(ep, k));
                 ++k;
             }
@@ -591,13 +624,14 @@ __device__ bool propagate(const SLds<K, C> &S, int mpad, int &tl, int nu, bool d
             tl += pre;
         } else {
         int k0 = 0;
+        snap_ready(S, nu);
         do {   // nu > 0: at least one step
             ph.count(15);
             const int k = k0 + ln;
             // lanes past nu read entry 0 (its variable is stamped with index 0
             // != k: never first).  Stale entries past nu are not safe to read:
             // an epoch can repeat across rounds, and so can (stamp, index).
-            const uint32_t code = (uint32_t)S.snap[k < nu ? k : 0];
+            const uint32_t code = snap_get(S, (uint32_t)(k < nu ? k : 0));
             const uint32_t v = code >> 1;
             // (one compare: its ballot folds into the v_cmp)
             const bool first = ts_first(S, v) == stamp(bep, (uint32_t)k);
@@ -1184,7 +1218,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     const int n = A.inst_nvars[b];
     const bool is_task = SPLIT && task >= 0;   // the unsplit form has no donated tasks
     int64_t *ctr = is_task ? slot_ref(A, task).h->ctr : A.counters + (int64_t)b * SATMI_NCOUNTERS;
-    bool bad = m > A.lay.mcap || n > A.lay.ncap || n < 0 || L > 65535 || (INC && L > A.occ_cap);
+    bool bad = m > A.lay.mcap || n > A.lay.ncap || n < 0 || L > 65535 || (INC && L > (sizeof(C) == 1 ? A.occ_cap : A.occ_lists));
     if (!bad) {
         // ---- stage: pack each clause's literal codes into one word
         for (int c = ln; c < mpad; c += 64) {
@@ -1599,10 +1633,14 @@ __global__ void __launch_bounds__(LVS ? 64 : 256, SATMI_SCAN_WAVES_PER_SIMD) dpl
     S.ftrail = (C *)(base + A.lay.ftrail);
     S.snap = (C *)(base + A.lay.scratch);
     S.plist = (uint32_t *)(base + A.lay.scratch);
+    S.scap = A.snap_lds;
+    uint16_t *const wreg = A.occ ? A.occ + ((size_t)blockIdx.x * (blockDim.x >> 6) + (size_t)wave) * (size_t)A.occ_cap
+                                 : nullptr;
+    S.snapg = (C *)(wreg ? wreg + A.occ_lists : nullptr);
     if constexpr (INC) {
         S.occ_off = (uint16_t *)(base + A.lay.occ_off);
         S.bm = (uint2 *)(base + A.lay.bm);
-        S.occ = A.occ + ((size_t)blockIdx.x * (blockDim.x >> 6) + (size_t)wave) * (size_t)A.occ_cap;
+        S.occ = wreg;
         for (int w = lane_id(); w < A.lay.nw; w += 64) S.bm[w].x = 0u;
         wave_sync();
     }
@@ -1645,6 +1683,8 @@ __global__ void __launch_bounds__(64, SATMI_SCAN_WAVES_PER_SIMD) dpll_fixed_kern
     S.ftrail = ftrail_s;
     S.snap = (uint8_t *)scratch_s;
     S.plist = scratch_s;
+    S.snapg = nullptr;   // byte codes: the whole snapshot in LDS
+    S.scap = FIXM + 4;
     S.occ_off = occ_off_s;
     S.bm = bm_s;
     S.occ = A.occ + (size_t)blockIdx.x * (size_t)A.occ_cap;
@@ -1663,10 +1703,14 @@ constexpr uint32_t FIX_LDS_BYTES = 4 * FIX_MCAP + 2 * (FIX_NCAP + 1) + 3 * 4 * (
 int lv_static_class(int K, int max_vars) {
     const int need = 2 * (max_vars + 1);
     if (K == 3) return need <= 256 ? 256 : 2 * (Pack<3>::MAXV + 1);
-    return 2 * (Pack<5>::MAXV + 1);
+    return need <= 512 ? 512 : 2 * (Pack<5>::MAXV + 1);   // 5-SAT n <= 255: 3.5 KB less per wave
 }
 
 uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+
+// snapshot entries kept in LDS: all with byte codes, at most 512 with 16-bit
+// codes (the rest in HBM: snap_put); M = clauses + 1
+uint32_t snap_lds_entries(uint32_t cb, uint32_t M) { return cb == 1 ? M : std::min(M, 512u); }
 
 int pick_k(int max_vars, int max_clause_len) {
     if (max_clause_len < 1 || max_clause_len > 5) return 0;
@@ -1686,11 +1730,15 @@ bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, bool inc, u
     lay->cls = o;     o = align16(o + (K == 3 ? 4u : 8u) * Mpad);
     lay->ts = o;      o = align16(o + 4 * N);
     lay->cnt = o;     o = align16(o + 8 * N);
-    lay->first = o;   o = align16(o + 4 * N);
+    // choose()'s flags alias the stamps when every first position + 1, (c << 3 |
+    // slot) + 1, stays <= 0x10000: below any stamp of an epoch >= 1 (as in
+    // dpll_fixed_kernel); larger formulas keep a separate array
+    if (max_clauses <= 8191) lay->first = lay->ts;
+    else { lay->first = o; o = align16(o + 4 * N); }
     lay->trail = o;   o = align16(o + cb * N);
     lay->fvar = o;    o = align16(o + cb * N);
     lay->ftrail = o;  o = align16(o + cb * N);
-    lay->scratch = o; o = align16(o + std::max(cb * M, 4 * N));
+    lay->scratch = o; o = align16(o + std::max(cb * snap_lds_entries(cb, M), 4 * N));
     lay->occ_off = o; o = align16(o + (inc ? 2 * (2 * N + 1) : 0u));
     lay->bm = o;      o = align16(o + (inc ? 8 * NW : 0u));
     lay->bytes = o;
@@ -1707,6 +1755,7 @@ const void *scan_fn(int K, int lvs) {   // occupancy queries: the split form (th
         if (lvs == 1024) return (const void *)dpll_scan_kernel<3, 1024, INC, true>;
         return (const void *)dpll_scan_kernel<3, 0, INC, true>;
     }
+    if (lvs == 512) return (const void *)dpll_scan_kernel<5, 512, INC, true>;
     return lvs ? (const void *)dpll_scan_kernel<5, 4096, INC, true> : (const void *)dpll_scan_kernel<5, 0, INC, true>;
 }
 const void *scan_fn(int K, int lvs, bool inc) { return inc ? scan_fn<true>(K, lvs) : scan_fn<false>(K, lvs); }
@@ -1781,6 +1830,8 @@ void launch_kernel(int K, int lvs, dim3 g, dim3 blk, uint32_t wg_lds, hipStream_
         hipLaunchKernelGGL((dpll_scan_kernel<3, 1024, INC, SPLIT>), g, blk, wg_lds, s, A);
     else if (K == 3)
         hipLaunchKernelGGL((dpll_scan_kernel<3, 0, INC, SPLIT>), g, blk, wg_lds, s, A);
+    else if (lvs == 512)
+        hipLaunchKernelGGL((dpll_scan_kernel<5, 512, INC, SPLIT>), g, blk, wg_lds, s, A);
     else if (lvs)
         hipLaunchKernelGGL((dpll_scan_kernel<5, 4096, INC, SPLIT>), g, blk, wg_lds, s, A);
     else
@@ -1858,6 +1909,8 @@ int dpll_scan_launch(const ScanLaunch &L) {
     A.work_counter = L.work_counter;
     A.occ = nullptr;
     A.occ_cap = 0;
+    A.occ_lists = 0;
+    A.snap_lds = P.fixed ? 0u : snap_lds_entries(P.lvs == 256 ? 1u : 2u, (uint32_t)lay.mcap + 1u);
     A.lay = lay;
     A.split = nullptr;
     // split only where the launch's tail matters: fewer than SPLIT_MAX_PER_WAVE
@@ -1900,13 +1953,16 @@ int dpll_scan_launch(const ScanLaunch &L) {
         SATMI_HIP(hipMemcpyAsync(p, &cfg, sizeof(cfg), hipMemcpyHostToDevice, L.stream));
         A.split = (SplitCfg *)p;
     }
-    if (L.inc) {
-        // occurrence lists: max_lits entries (rounded to 128 B) per resident wave
-        A.occ_cap = (std::max(L.max_lits, 1) + 63) & ~63;
+    // per resident wave: occurrence lists (max_lits entries, rounded to 128 B),
+    // then the snapshot entries LDS does not hold (<= one per clause)
+    if (L.inc) A.occ_lists = (std::max(L.max_lits, 1) + 63) & ~63;
+    const int snap_ovf = (!P.fixed && (uint32_t)lay.mcap + 1u > A.snap_lds) ? ((lay.mcap + 1 - (int)A.snap_lds) + 63) & ~63 : 0;
+    A.occ_cap = A.occ_lists + snap_ovf;
+    if (A.occ_cap > 0) {
         const size_t bytes = (size_t)grid * (size_t)waves_per_wg * (size_t)A.occ_cap * sizeof(uint16_t);
         A.occ = L.occ_alloc ? L.occ_alloc(bytes) : nullptr;
         if (!A.occ) {
-            set_error("dpll_scan_launch: no occurrence-list scratch for the incremental kernel");
+            set_error("dpll_scan_launch: no per-wave scratch (occurrence lists / snapshot)");
             return SATMI_ERR_NOMEM;
         }
     }

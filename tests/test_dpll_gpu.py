@@ -261,6 +261,49 @@ def test_scan_kernel_full_size_matches_general():
         assert (rs.sol_lits == rg.sol_lits).all()
 
 
+def _mass_unit_formulas(seed, count):
+    """16-bit-code formulas (n > 127) whose snapshots exceed the 512 entries the
+    scan kernel keeps in LDS (the rest go to the wave's HBM scratch): a hub
+    variable in 520-900 binary clauses [-1, l] (its True branch makes them all
+    unit at once) or 520-700 unit clauses at the root, plus random 3-clauses.
+    The unit literals repeat (a variable's first occurrence wins, some first
+    occurrences lie past entry 512) with one sign per variable (the whole
+    snapshot is assigned: every clause holds a literal of that sign) or with
+    random signs (a conflict cuts it)."""
+    rng = random.Random(seed)
+    fs = []
+    for i in range(count):
+        n = rng.randint(130, 250)
+        sign = [1 if rng.random() < 0.5 else -1 for _ in range(n + 1)]
+        lit = lambda: rng.randint(2, n) * (1 if rng.random() < 0.5 else -1)   # noqa: E731
+        ulit = (lambda: (lambda v: v * sign[v])(rng.randint(2, n))) if i % 2 == 0 else lit   # noqa: E731
+        if i % 3 == 2:
+            f = [[ulit()] for _ in range(rng.randint(520, 700))]
+        else:   # the hub occurs both ways (not pure), and most in the binary clauses: branched on first
+            f = [[-1, ulit()] for _ in range(rng.randint(520, 900))] + [[1, lit(), lit()] for _ in range(20)]
+        f += [[ulit(), lit(), lit()] for _ in range(rng.randint(n // 2, n))]
+        rng.shuffle(f)
+        fs.append(f)
+    return fs
+
+
+def test_snapshot_past_lds_entries_matches_general_and_oracle():
+    fs = _mass_unit_formulas(91, 36)
+    rg = _run_policy(fs, _capi.KERNEL_GENERAL, max_solutions=1, sol_cap=1, node_limit=3000)
+    for kern in (_capi.KERNEL_SCAN, _capi.KERNEL_INC):
+        rs = _run_policy(fs, kern, max_solutions=1, sol_cap=1, node_limit=3000)
+        assert (rs.status == rg.status).all(), kern
+        assert (rs.counters[:, :7] == rg.counters[:, :7]).all(), kern
+        for b in range(len(fs)):
+            assert rs.solutions(b) == rg.solutions(b), (kern, b)
+    assert (rg.counters[:, 2] > 0).all()   # unit propagations happened in every instance
+    for b in range(0, len(fs), 3):
+        o = oracle.dpll(fs[b], "sound", max_solutions=1, sol_cap=1, node_limit=3000)
+        for key in CTR:
+            assert rs.counter_dict(b)[key] == o["counters"][key], (key, b)
+        assert rs.solutions(b) == o["solutions"][:1]
+
+
 def test_scan_policy_rejects_ineligible():
     f = [[1, 2], [-1, 2], []]
     for kern in (_capi.KERNEL_SCAN, _capi.KERNEL_INC):
