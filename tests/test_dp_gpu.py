@@ -132,3 +132,19 @@ def test_concurrent_solves_from_threads():
     for f, o in zip(fs[:2], want[:2]):
         r = eliminate(f, record=True)
         assert (r["result"], r["vars"]) == (o["result"], o["vars"]) and r["clauses"] == o["clauses"][:_completed(o)]
+
+
+def test_bench_random_unsat_set_matches_oracle():
+    """The bench's configs[3] `rand-dp` set (16 random 3-SAT formulas n=16,
+    m=96, seed 7002): verdicts, eliminated variables and every clause list."""
+    batch = cnf.uniform_ksat(16, 16, 96, 3, seed=7002)
+    unsat = 0
+    for b in range(16):
+        f = batch.instance(b)
+        o = oracle.dp(f, record=True)
+        r = eliminate(f, record=True, time_limit=60.0)
+        assert r["result"] == o["result"], b
+        assert r["vars"] == o["vars"], b
+        assert r["clauses"] == o["clauses"][:_completed(o)], b
+        unsat += r["result"] == 0
+    assert unsat >= 12   # past the threshold: the set is mostly UNSAT

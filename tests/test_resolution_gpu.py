@@ -222,3 +222,16 @@ def test_regrowth_call_reports_each_pass_once():
     assert r1 == r2
     assert (s1["pairs"], s1["candidates"]) == (s2["pairs"], s2["candidates"])
     assert s1["pair_ms"] < 1.6 * s2["pair_ms"] + 0.05
+
+
+def test_bench_random_unsat_set_matches_oracle():
+    """The bench's configs[3] `rand-res` set (16 random 3-SAT formulas n=7,
+    m=49, seed 7001): the first two, every pass's clause set against the oracle."""
+    batch = cnf.uniform_ksat(16, 7, 49, 3, seed=7001)
+    for b in (0, 1):
+        f = batch.instance(b)
+        o = oracle.resolution(f, record=True)
+        r = resolve(f, record=True, time_limit=60.0)
+        assert r["result"] == o["result"]
+        assert list(r["pass_new"]) == list(o["pass_new"])
+        assert [sorted(p) for p in r["clauses"]] == [sorted(p) for p in o["clauses"]]
