@@ -25,13 +25,16 @@ child process after the headline -- the line's `configs` object):
     uf250      configs[4]: uf250-1065 shape (random 3-SAT n=250, m=1065),
                node-capped search (--node-limit, default 20,000 calls/instance)
     5sat-n200  configs[4]: random 5-SAT n=200 at the 5-SAT threshold
-               (alpha=21.117, m=4,223): long clauses, 1 wave per CU of LDS
+               (alpha=21.117, m=4,223): long clauses, 4 waves per CU of LDS
     php-dp     configs[3]: Davis-Putnam elimination of pigeonhole PHP(6,5)
                (30 variables, 81 clauses; every step's resolvents, tautology
                and subsumption filter on the GPU) -- solves/s
     php-res    configs[3]: resolution saturation of PHP(4,3) (pair kernel +
                hash dedup), its first 4 passes (171,392 derived clauses; the
                5th pass would resolve 1.5e10 pairs) -- derived clauses/s
+    rand-res / rand-dp  configs[3]'s small random UNSAT sets: 16 random 3-SAT
+               formulas (n=7, m=49 / n=16, m=96) saturated by resolution /
+               eliminated by Davis-Putnam to the end -- formulas/s
     cdcl       the reference's CDCLSolver (REF.py:217-384) on 32,768 menu-sized
                formulas (generate_large_formula(80, 3, 15), REF.py:21-29, the
                shape of rezultat.txt:178-188), <= 10,000 iterations each --
@@ -545,30 +548,38 @@ def run_dpll(args, world, rank, local):
     return out, host
 
 
-DP_MIN_KERNEL_US = 0.64   # shortest DP kernel in the r04 kernel trace (a launch with nothing to do)
-
-
-def dp_roofline(stats, solves_per_s):
+def dp_roofline(stats, solves_per_s, floor_us):
     """Davis-Putnam (php-dp): a solve is a chain of dependent kernel launches
     (csrc/dp.hip: DP_LAUNCHES_PER_STEP per elimination step, 30 steps for
-    PHP(6,5)) whose sizes live on the device, replayed from a HIP graph; most
+    PHP(6,5)) whose sizes live on the device, replayed from HIP graphs; most
     steps are small, so the chain's latency binds, not a pipe or HBM.
-    achieved = launches completed per second; peak = one launch per the
-    shortest kernel duration measured in the kernel trace
-    (profiles/r04/dp_kernel_stats.txt: a launch with no work); device_ms = the
-    steps' device time (HIP events) per solve."""
+    achieved = launches completed per second; peak = the launch rate of an
+    EMPTY dependent chain of the same length replayed from a HIP graph on this
+    GPU, measured by the caller (`floor_us`, satmi_launch_chain_floor: one-block
+    kernels, no work) -- the rate no chain of that many launches can beat;
+    device_ms = the steps' device time (HIP events) per solve."""
     if not stats:
         return None
     launches = sum(s["launches"] for s in stats) / len(stats)
     dms = sum(s["device_ms"] for s in stats) / len(stats)
     ach = launches * solves_per_s
-    peak = 1e6 / DP_MIN_KERNEL_US
+    peak = 1e6 / floor_us
     return {"bound": "launch-latency", "achieved": ach, "peak": peak, "unit": "launches/s", "frac": ach / peak,
+            "peak_source": "measured: an empty chain of as many dependent one-block launches replayed from a HIP "
+                           "graph (satmi_launch_chain_floor)", "floor_us_per_launch": floor_us,
             "traffic": None, "kernel": "dp step chain (9 kernels per elimination step)",
             "launches_per_solve": launches, "device_ms_per_solve": dms,
             "us_per_launch": dms * 1e3 / launches if launches else None,
             "subset_tests_per_solve": sum(s["subset_tests"] for s in stats) / len(stats),
             "new_clauses_per_solve": sum(s["new_clauses"] for s in stats) / len(stats), "key_words": stats[-1]["words"]}
+
+
+def dp_launch_floor(stats):
+    """satmi_launch_chain_floor over a chain as long as a solve's (after the timed region)."""
+    if not stats:
+        return None
+    n = max(1, int(round(sum(s["launches"] for s in stats) / len(stats))))
+    return _capi.launch_chain_floor(n, reps=20)
 
 
 def saturation_roofline(stats, nvars):
@@ -662,7 +673,7 @@ def run_saturation(args, world, rank, local):
                       "preset": args.workload, "parallelism": f"replicas x{world}", "concurrent_solves": T},
            "result": last["result"], "passes_or_steps": last.get("passes", last.get("steps")),
            "roofline": saturation_roofline(stats, len({abs(l) for c in f for l in c})) if args.workload == "php-res" else
-           dp_roofline(stats, done * world / elapsed)}
+           dp_roofline(stats, done * world / elapsed, dp_launch_floor(stats))}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps:
         # the oracle on the same formula: checked against the GPU, then replicas

@@ -176,6 +176,13 @@ int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const int32_t *h_li
                   int trace_cap, int32_t *h_steps, int32_t *h_rec_lits, int64_t rec_lit_cap,
                   int64_t *h_rec_clause_off, int64_t rec_clause_cap, int64_t *h_rec_step_off, int rec_step_cap);
 
+/* The floor of a chain of dependent kernel launches replayed from a HIP graph
+ * on this device: `launches` one-block kernels captured in order on one
+ * stream, the graph replayed `reps` times; *us_per_launch = the time per
+ * launch.  The Davis-Putnam roofline (a solve is a chain of ~280 dependent
+ * launches) prices its launches/s against this measured floor. */
+int satmi_launch_chain_floor(int launches, int reps, double *us_per_launch);
+
 /* Work of the calling thread's last satmi_dp_host call: elimination steps,
  * subset tests performed by the unique_new filter (REF.py:122-125), new
  * (non-tautological) resolvents, kernel launches enqueued for the steps, key

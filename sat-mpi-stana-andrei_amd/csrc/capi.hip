@@ -17,6 +17,12 @@ int hip_fail(hipError_t e, const char *what) {
     return SATMI_ERR_HIP;
 }
 
+// One link of an empty dependent chain (satmi_launch_chain_floor): a single
+// vector load + store keeps the launch from being trivially empty.
+__global__ void chain_link_kernel(uint32_t *p) {
+    if (threadIdx.x == 0) p[0] += 1u;
+}
+
 }  // namespace satmi
 
 using namespace satmi;
@@ -70,6 +76,47 @@ int satmi_memcpy_d2h(void *h_dst, const void *d_src, uint64_t bytes, void *strea
 int satmi_stream_synchronize(void *stream) {
     SATMI_HIP(hipStreamSynchronize((hipStream_t)stream));
     return SATMI_OK;
+}
+
+int satmi_launch_chain_floor(int launches, int reps, double *us_per_launch) {
+    if (launches < 1 || reps < 1 || !us_per_launch) {
+        set_error("satmi_launch_chain_floor: bad arguments");
+        return SATMI_ERR_ARG;
+    }
+    hipStream_t s = nullptr;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    uint32_t *d = nullptr;
+    int rc = SATMI_OK;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&d, 256);
+    if (e == hipSuccess) e = hipMemsetAsync(d, 0, 256, s);
+    if (e == hipSuccess) e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+        for (int i = 0; i < launches; ++i) hipLaunchKernelGGL(chain_link_kernel, dim3(1), dim3(64), 0, s, d);
+        e = hipStreamEndCapture(s, &g);
+    }
+    if (e == hipSuccess) e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipGraphLaunch(ge, s);   // warm-up replay
+    if (e == hipSuccess) e = hipEventRecord(e0, s);
+    for (int r = 0; e == hipSuccess && r < reps; ++r) e = hipGraphLaunch(ge, s);
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess) *us_per_launch = (double)ms * 1e3 / ((double)launches * reps);
+    else rc = hip_fail(e, "satmi_launch_chain_floor");
+    if (e1) (void)hipEventDestroy(e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (ge) (void)hipGraphExecDestroy(ge);
+    if (g) (void)hipGraphDestroy(g);
+    if (s) (void)hipStreamSynchronize(s);
+    if (d) (void)hipFree(d);
+    if (s) (void)hipStreamDestroy(s);
+    return rc;
 }
 
 }  // extern "C"

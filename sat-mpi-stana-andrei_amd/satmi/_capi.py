@@ -32,7 +32,7 @@ EXPORTED = (
     "satmi_resolution_last_stats", "satmi_resolution_last_clock", "satmi_dpll_set_split", "satmi_dpll_split_stats",
     "satmi_dp_last_stats",
     "satmi_cdcl_batch_host", "satmi_dpll_set_split_warmup", "satmi_resolution_debug_cand_bytes",
-    "satmi_dp_trim", "satmi_resolution_trim", "satmi_cdcl_last_stats",
+    "satmi_dp_trim", "satmi_resolution_trim", "satmi_cdcl_last_stats", "satmi_launch_chain_floor",
 )
 
 
@@ -135,6 +135,7 @@ def load():
     L.satmi_resolution_last_stats.argtypes = [i64p, i64p, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)]
     L.satmi_resolution_last_clock.argtypes = [ctypes.POINTER(ctypes.c_double)]
+    L.satmi_launch_chain_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     L.satmi_dp_host.argtypes = [
         ctypes.c_int, i32p, i32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, i32p, i32p, ctypes.c_int, i32p,
         i32p, ctypes.c_int64, i64p, ctypes.c_int64, i64p, ctypes.c_int]
@@ -173,3 +174,13 @@ def require_gpu():
     if rc != OK or n.value < 1:
         raise SatmiError("no HIP device visible: the satmi solvers run on MI355X only (no CPU fallback)")
     return n.value
+
+
+def launch_chain_floor(launches, reps=20):
+    """Microseconds per launch of a chain of `launches` dependent one-block
+    kernels replayed from a HIP graph (satmi_launch_chain_floor)."""
+    L = load()
+    require_gpu()
+    us = ctypes.c_double(0.0)
+    check(L.satmi_launch_chain_floor(int(launches), int(reps), ctypes.byref(us)), "satmi_launch_chain_floor")
+    return us.value

@@ -4,8 +4,9 @@
   is charged against the issue pipe its SQ passes found binding
   (profiles/sq_issue.json "php-res_B1", per step) over the run's live kernel
   time, with the step's HBM bytes beside it;
-* php-dp: a solve is a chain of dependent launches, priced against one launch
-  per the shortest kernel of the trace (bench.DP_MIN_KERNEL_US)."""
+* php-dp: a solve is a chain of dependent launches, priced against the
+  launch rate of an empty chain of the same length measured on the GPU
+  (satmi_launch_chain_floor; a fixed floor here)."""
 import bench
 
 
@@ -34,13 +35,14 @@ def test_saturation_roofline_is_the_issue_roofline_of_the_pass_kernel():
 
 def test_dp_roofline_prices_the_launch_chain():
     st = [{"launches": 280, "device_ms": 3.0, "subset_tests": 10, "new_clauses": 4, "words": 2}] * 3
-    r = bench.dp_roofline(st, solves_per_s=300.0)
+    r = bench.dp_roofline(st, solves_per_s=300.0, floor_us=2.0)
     assert r["bound"] == "launch-latency" and r["unit"] == "launches/s"
     assert r["achieved"] == 280 * 300.0
-    assert r["peak"] == 1e6 / bench.DP_MIN_KERNEL_US
+    assert r["peak"] == 1e6 / 2.0 and r["floor_us_per_launch"] == 2.0
+    assert r["peak_source"].startswith("measured")
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
     assert abs(r["us_per_launch"] - 3.0e3 / 280) < 1e-9
-    assert bench.dp_roofline([], 1.0) is None
+    assert bench.dp_roofline([], 1.0, 2.0) is None
 
 
 def test_saturation_roofline_prices_the_pipes_at_the_live_clock():

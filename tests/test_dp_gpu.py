@@ -148,3 +148,19 @@ def test_bench_random_unsat_set_matches_oracle():
         assert r["clauses"] == o["clauses"][:_completed(o)], b
         unsat += r["result"] == 0
     assert unsat >= 12   # past the threshold: the set is mostly UNSAT
+
+
+def test_launch_chain_floor():
+    """satmi_launch_chain_floor (the php-dp roofline's peak): an empty chain of
+    dependent one-block launches replayed from a HIP graph takes a positive,
+    microsecond-scale time per launch, and no less per launch than a solve's
+    real kernels (which do work)."""
+    from satmi import _capi
+    from satmi.dp import last_stats
+    floor = _capi.launch_chain_floor(280, reps=5)
+    assert 0.05 < floor < 50.0
+    eliminate(cnf.pigeonhole(5))
+    st = last_stats()
+    assert st["device_ms"] * 1e3 / st["launches"] >= floor
+    with pytest.raises(_capi.SatmiError):
+        _capi.launch_chain_floor(0)
