@@ -101,6 +101,11 @@ LEGS = [
     ("cdcl", "cdcl", ["--steps", "3", "--warmup", "1"]),
     ("cdcl 4 threads", "cdcl", ["--steps", "3", "--warmup", "1", "--threads", "4"]),
 ]
+# legs run by a second child with a hardware queue per stream (GPU_MAX_HW_QUEUES,
+# read at HIP start); the others keep HIP's default of 4 queues -- more queues
+# cost concurrent host threads (php-dp with 8 threads: 1.09 k solves/s with 4
+# queues, 0.71 k with 17; tools/hwq_sweep.sh)
+HWQ17_LEGS = ("configs[1] 16 streams",)
 
 
 def parse(argv=None):
@@ -122,6 +127,7 @@ def parse(argv=None):
                    help="searches solved to the end: the CPU sample's node cap (its rate scaled to instances/s)")
     p.add_argument("--no-legs", action="store_true", help="only the headline workload (no `configs` object)")
     p.add_argument("--legs-only", action="store_true", help=argparse.SUPPRESS)   # the child of the default run
+    p.add_argument("--legs-hwq17", action="store_true", help=argparse.SUPPRESS)  # ... its HWQ17_LEGS child
     p.add_argument("--leg-cpu-seconds", type=float, default=4.0, help="CPU baseline budget of each leg")
     p.add_argument("--profile-steps", action="store_true", help="no warmup/cpu leg (for rocprofv3 runs)")
     p.add_argument("--kernel", choices=("auto", "inc", "scan", "general"), default="auto",
@@ -881,11 +887,14 @@ def run_one(args, world, rank, local):
 
 
 def legs_main(args):
-    """The default run's child: every other BASELINE config, short, one JSON
-    object {name: compact line}.  A child process so that its 16-stream leg
-    gets a hardware queue per stream (GPU_MAX_HW_QUEUES, read at HIP start)."""
+    """The default run's children: every other BASELINE config, short, one JSON
+    object {name: compact line}.  Child processes so that the 16-stream leg
+    gets a hardware queue per stream (GPU_MAX_HW_QUEUES, read at HIP start:
+    --legs-hwq17 runs HWQ17_LEGS, the other child the rest)."""
     out = {}
     for name, wl, extra in LEGS:
+        if (name in HWQ17_LEGS) != args.legs_hwq17:
+            continue
         a = parse(["--workload", wl, "--cpu-seconds", str(args.leg_cpu_seconds), "--seed", str(args.seed)] + extra)
         t = time.perf_counter()
         r = run_one(a, 1, 0, 0)
@@ -911,16 +920,21 @@ def main():
     legs = (world == 1 and not args.no_legs and not args.profile_steps and args.workload == "3sat-n100"
             and args.total == WORKLOADS["3sat-n100"][0])
     if legs and rank == 0:
-        env = dict(os.environ, GPU_MAX_HW_QUEUES="17")
-        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--legs-only", "--seed", str(args.seed),
-                            "--leg-cpu-seconds", str(args.leg_cpu_seconds)]
-                           + (["--no-cpu-baseline"] if args.no_cpu_baseline else []),
-                           capture_output=True, text=True, env=env)
-        if r.returncode != 0:
-            raise SystemExit(f"bench: secondary configs failed:\n{r.stderr[-4000:]}")
-        out["configs"] = json.loads(r.stdout.strip().splitlines()[-1])
-        out["configs_note"] = ("the other BASELINE configs, measured after the headline by a child process "
-                               "(bench.py --legs-only, GPU_MAX_HW_QUEUES=17) with the same harness; "
+        got = {}
+        for hwq in (False, True):
+            env = dict(os.environ, GPU_MAX_HW_QUEUES="17") if hwq else dict(os.environ)
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--legs-only", "--seed", str(args.seed),
+                                "--leg-cpu-seconds", str(args.leg_cpu_seconds)]
+                               + (["--legs-hwq17"] if hwq else [])
+                               + (["--no-cpu-baseline"] if args.no_cpu_baseline else []),
+                               capture_output=True, text=True, env=env)
+            if r.returncode != 0:
+                raise SystemExit(f"bench: secondary configs failed:\n{r.stderr[-4000:]}")
+            got.update(json.loads(r.stdout.strip().splitlines()[-1]))
+        out["configs"] = {name: got[name] for name, _, _ in LEGS if name in got}
+        out["configs_note"] = ("the other BASELINE configs, measured after the headline by two child processes "
+                               "(bench.py --legs-only; the 16-stream leg with GPU_MAX_HW_QUEUES=17, the rest with "
+                               "HIP's default queues) with the same harness; "
                                "configs[1] ('4,096 instances, n=50, on 1 MI355X') is answered by the 2-stream "
                                "leg: batches of 4,096 solved back to back, the next batch's waves taking the CUs "
                                "the current batch's tail leaves idle (at most 8,192 instances resident); the "

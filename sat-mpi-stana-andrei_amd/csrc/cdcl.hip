@@ -353,6 +353,7 @@ __device__ __forceinline__ bool lit_false(const St &S, int lit) {
 constexpr int CDCL_LITS_AHEAD = 4;   // a member's first literals read at once
 
 __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
+    __shared__ __attribute__((aligned(4))) uint8_t own8[256];   // window slot -> owning key lane (one-wave groups)
     const int ln = lane_id();
     CDCL_CLK(S, 3);
     const int nk0 = q.nk;   // list(self.watch_list): keys created during the pass are not visited
@@ -362,28 +363,32 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
         const int size = fl ? S.wmask[kk] + 1 : 0;
         const int incl = wave_incl_scan(size);
         const int total = lane63(incl), excl = incl - size;
-        const uint64_t fm = __ballot(fl);
 #ifdef SATMI_CDCL_PHASES
+        const uint64_t fm = __ballot(fl);
         if (ln == 0) S.clk[6] += (uint64_t)__popcll(fm);
 #endif
         for (int g0 = 0, nch; g0 < total; g0 += 64 * nch) {
             nch = min(4, (total - g0 + 63) >> 6);   // one window when the stream fits 256 slots
             // the stream slot g of (u, lane): its key (the last false key whose
-            // table starts at or before g) and the slot in that table
+            // table starts at or before g) and the slot in that table.  Each
+            // false key marks its table's first slot in an LDS byte map of the
+            // window; a prefix max over the slots carries every mark to the
+            // slots after it (tables come in key order, so the latest mark is
+            // the owner) -- no serial loop over the false keys
+            ((uint32_t *)own8)[ln] = 0xFFFFFFFFu;   // the window's 256 bytes: no mark
+            if (fl && excl >= g0 && excl < g0 + 64 * nch) own8[excl - g0] = (uint8_t)ln;
+            const uint64_t before = __ballot(fl && excl < g0);   // keys whose tables began in earlier windows
+            int carry = before ? 63 - __builtin_clzll(before) : -1;
             int own[4], ex[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) own[u] = ex[u] = 0;
-            for (uint64_t m = fm; m; m &= m - 1) {
-                const int bl = __builtin_ctzll(m);
-                const int eb = __builtin_amdgcn_readlane(excl, bl);
-                if (eb >= g0 + 64 * nch) break;   // keys past the window
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (u < nch) {
-                        const bool after = g0 + 64 * u + ln >= eb;
-                        own[u] = after ? bl : own[u];
-                        ex[u] = after ? eb : ex[u];
-                    }
+            for (int u = 0; u < 4; ++u) {
+                own[u] = ex[u] = 0;
+                if (u < nch) {
+                    const int m8 = own8[64 * u + ln];
+                    const int o = wave_incl_max(max(m8 == 0xFF ? -1 : m8, carry));
+                    carry = __builtin_amdgcn_readlane(o, 63);
+                    own[u] = max(o, 0);
+                    ex[u] = __builtin_amdgcn_ds_bpermute(own[u] << 2, excl);
                 }
             }
             int32_t x[4], lit[4];
