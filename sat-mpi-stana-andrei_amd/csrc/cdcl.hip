@@ -350,7 +350,15 @@ __device__ __forceinline__ bool lit_false(const St &S, int lit) {
 // order (they may create keys and resize tables).  A launch's long
 // solves are latency-bound chains of dependent memory reads, and one window
 // covers the false lists of a typical pass at once.
-constexpr int CDCL_LITS_AHEAD = 4;   // a member's first literals read at once
+// a member's first literals read at once (the menu formulas' clauses and their
+// learned copies have 3; longer clauses read the rest one at a time): 3 measured
+// +5 % over 4 (profiles/r05/steps/cdcl_owner_scan_ab.txt)
+#ifndef CDCL_LITS_AHEAD
+#define CDCL_LITS_AHEAD 3
+#endif
+#ifndef CDCL_WCH
+#define CDCL_WCH 4          // 64-slot chunks per propagate window (reads in flight)
+#endif
 
 __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
     __shared__ __attribute__((aligned(4))) uint8_t own8[256];   // window slot -> owning key lane (one-wave groups)
@@ -368,7 +376,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
         if (ln == 0) S.clk[6] += (uint64_t)__popcll(fm);
 #endif
         for (int g0 = 0, nch; g0 < total; g0 += 64 * nch) {
-            nch = min(4, (total - g0 + 63) >> 6);   // one window when the stream fits 256 slots
+            nch = min(CDCL_WCH, (total - g0 + 63) >> 6);   // one window when the stream fits 256 slots
             // the stream slot g of (u, lane): its key (the last false key whose
             // table starts at or before g) and the slot in that table.  Each
             // false key marks its table's first slot in an LDS byte map of the
@@ -379,9 +387,9 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             if (fl && excl >= g0 && excl < g0 + 64 * nch) own8[excl - g0] = (uint8_t)ln;
             const uint64_t before = __ballot(fl && excl < g0);   // keys whose tables began in earlier windows
             int carry = before ? 63 - __builtin_clzll(before) : -1;
-            int own[4], ex[4];
+            int own[CDCL_WCH], ex[CDCL_WCH];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < CDCL_WCH; ++u) {
                 own[u] = ex[u] = 0;
                 if (u < nch) {
                     const int m8 = own8[64 * u + ln];
@@ -391,10 +399,10 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                     ex[u] = __builtin_amdgcn_ds_bpermute(own[u] << 2, excl);
                 }
             }
-            int32_t x[4], lit[4];
-            int at[4];
+            int32_t x[CDCL_WCH], lit[CDCL_WCH];
+            int at[CDCL_WCH];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {   // up to four table reads in flight
+            for (int u = 0; u < CDCL_WCH; ++u) {   // up to four table reads in flight
                 const int g = g0 + 64 * u + ln;
                 const bool in = u < nch && g < total;
                 const int k = k0 + own[u];
@@ -402,10 +410,10 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
                 lit[u] = in ? S.klit[k] : 0;
                 x[u] = in ? S.pool[at[u]] : WS_EMPTY;
             }
-            bool act[4];
-            int jb[4], je[4];
+            bool act[CDCL_WCH];
+            int jb[CDCL_WCH], je[CDCL_WCH];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < CDCL_WCH; ++u) {
                 act[u] = x[u] != WS_EMPTY && x[u] != WS_DUMMY;
                 jb[u] = act[u] ? S.coff[x[u] - 1] : 0;
                 je[u] = act[u] ? S.coff[x[u]] : 0;
@@ -414,14 +422,14 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             // replacement watch: the clause's first literal other than lit that
             // is free or true (REF.py:279-286); the first CDCL_LITS_AHEAD of
             // every member are read together
-            int r[4];
-            int o[4][CDCL_LITS_AHEAD];
+            int r[CDCL_WCH];
+            int o[CDCL_WCH][CDCL_LITS_AHEAD];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < CDCL_WCH; ++u)
 #pragma unroll
                 for (int t = 0; t < CDCL_LITS_AHEAD; ++t) o[u][t] = jb[u] + t < je[u] ? S.lits[jb[u] + t] : lit[u];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < CDCL_WCH; ++u) {
                 r[u] = 0;
 #pragma unroll
                 for (int t = 0; t < CDCL_LITS_AHEAD; ++t) {
@@ -445,7 +453,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             int cu = 4, cl = 64;
             int64_t conflict = -1;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < CDCL_WCH; ++u) {
                 const uint64_t nm = __ballot(act[u] && r[u] == 0);
                 if (cu == 4 && nm) {
                     cu = u;
@@ -460,7 +468,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             int nmv = 0;
 #endif
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < CDCL_WCH; ++u) {
                 const bool mv = act[u] && r[u] != 0 && (u < cu || (u == cu && ln < cl));
                 if (mv) S.pool[at[u]] = WS_DUMMY;
                 uint64_t mm = __ballot(mv);
@@ -480,7 +488,7 @@ __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
             {   // diagnostic counts: moves, members read
                 int na = 0;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) na += __popcll(__ballot(act[u]));
+                for (int u = 0; u < CDCL_WCH; ++u) na += __popcll(__ballot(act[u]));
                 if (ln == 0) {
                     S.clk[4] += (uint64_t)nmv;
                     S.clk[5] += (uint64_t)na;
