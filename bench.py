@@ -72,7 +72,7 @@ FIX_NCAP, FIX_MCAP = 127, 448  # dpll_fixed_kernel's shape class (csrc/dpll_scan
 WORKLOADS = {
     "3sat-n100": (262144, 100, 4.26, 3, 0, "configs[2]"),
     "3sat-n50": (4096, 50, 4.26, 3, 0, "configs[1]"),
-    "uf250": (6656, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,328 resident waves (13 / CU)
+    "uf250": (7680, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,840 resident waves (15 / CU)
     "5sat-n200": (2048, 200, 21.117, 5, 20000, "configs[4]"),  # 2 x the 1,024 resident waves (4 / CU)
 }
 # configs[3] presets: (holes, resolution passes) -- one formula per step, host-array C ABI

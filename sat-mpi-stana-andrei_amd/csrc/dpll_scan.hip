@@ -188,6 +188,48 @@ __device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return
 // never the product) each issued twice -- see dpll_scan_access.h.
 #include "dpll_scan_access.h"
 
+// Per-literal-code counters (the counting pass, the occurrence-list build).
+// One word per code, except for 3-literal clauses with 16-bit codes (n = 128 ..
+// 511): the two codes of a variable share a word, code 2v in the low half (a
+// count is at most the clause count, <= 65,534), which halves the array --
+// uf250 fits 15 searches per CU instead of 13 (+10 %).  (5-SAT n=200 gains no
+// residency from it and pays the packing's shifts: one word per code there.)
+template <int K, typename C>
+constexpr bool cnt_packed() { return sizeof(C) == 2 && K == 3; }
+template <int K, typename C>
+__device__ __forceinline__ void cnt_inc(const SLds<K, C> &S, uint32_t code, uint32_t inc) {
+    if constexpr (!cnt_packed<K, C>()) atomicAdd(&S.cnt[code], inc);
+    else atomicAdd(&S.cnt[code >> 1], inc << ((code & 1u) << 4));
+}
+template <int K, typename C>
+__device__ __forceinline__ uint32_t cnt_fetch_inc(const SLds<K, C> &S, uint32_t code) {   // the count before
+    if constexpr (!cnt_packed<K, C>()) {
+        return atomicAdd(&S.cnt[code], 1u);
+    } else {
+        const uint32_t sh = (code & 1u) << 4;
+        return (atomicAdd(&S.cnt[code >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    }
+}
+template <int K, typename C>
+__device__ __forceinline__ uint32_t cnt_get(const SLds<K, C> &S, uint32_t code) {
+    if constexpr (!cnt_packed<K, C>()) return S.cnt[code];
+    else return (S.cnt[code >> 1] >> ((code & 1u) << 4)) & 0xFFFFu;
+}
+template <int K, typename C>
+__device__ __forceinline__ uint2 cnt_pair(const SLds<K, C> &S, uint32_t v) {   // codes 2v, 2v + 1
+    if constexpr (!cnt_packed<K, C>()) {
+        return ((const uint2 *)S.cnt)[v];
+    } else {
+        const uint32_t w = S.cnt[v];
+        return make_uint2(w & 0xFFFFu, w >> 16);
+    }
+}
+template <int K, typename C>
+__device__ __forceinline__ void cnt_clear_var(const SLds<K, C> &S, uint32_t v) {
+    if constexpr (!cnt_packed<K, C>()) ((uint2 *)S.cnt)[v] = make_uint2(0u, 0u);
+    else S.cnt[v] = 0u;
+}
+
 
 // Apply f(c, w, x) to every clause c (w its packed word, x[j] the state byte of
 // its slot j), one 64-clause chunk per lane step; the loads of U chunks are
@@ -697,7 +739,7 @@ __device__ int scan_counts(const SLds<K, C> &S, int mpad) {
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const uint32_t code = field<K>(w, j);
-                atomicAdd(&S.cnt[code], x[j]);
+                cnt_inc(S, code, x[j]);
                 dup_count(S, code);
             }
         }
@@ -789,7 +831,7 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
         const int v = v0 + ln;
         const uint32_t vc = (uint32_t)min(v, n);
         const bool live = (v <= n) & var_free(S.lv, vc);
-        const uint2 c = ((const uint2 *)S.cnt)[vc];   // the counts of codes 2v, 2v + 1
+        const uint2 c = cnt_pair(S, vc);   // the counts of codes 2v, 2v + 1
         const uint32_t p = c.x, q = c.y;
         lmax = live ? max(lmax, p + q) : lmax;
         npure += __popcll(__ballot(live & ((p + q) != 0u) & ((p == 0u) | (q == 0u))));
@@ -808,7 +850,7 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
         const int v = v0 + ln;
         const uint32_t vc = (uint32_t)min(v, n);
         const bool live = (v <= n) & var_free(S.lv, vc);
-        const uint2 c = ((const uint2 *)S.cnt)[vc];
+        const uint2 c = cnt_pair(S, vc);
         const uint32_t p = c.x, q = c.y;
         const bool pure = live & ((p + q) != 0u) & ((p == 0u) | (q == 0u));
         const bool cand = live & (p + q == maxc);
@@ -817,7 +859,7 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
         ncand += __popcll(cm);
         const uint32_t vw = v <= n ? vc : 0u;
         S.first[vw] = npure ? (pure ? NONE32 : 0u) : (cand ? 1u : 0u);
-        ((uint2 *)S.cnt)[vw] = make_uint2(0u, 0u);   // cleared for the next scan
+        cnt_clear_var(S, vw);   // cleared for the next scan
     };
     if constexpr (sizeof(C) == 1) {
         if (n >= 1) flag_step(1);
@@ -825,7 +867,7 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
     } else {
         for (int v0 = 1; v0 <= n; v0 += 64) flag_step(v0);
     }
-    ((uint2 *)S.cnt)[0] = make_uint2(0u, 0u);   // variable 0: the padding slots' counts (never read)
+    cnt_clear_var(S, 0u);   // variable 0: the padding slots' counts (never read)
     S.first[0] = 0u;
     wave_sync();
     uint32_t best = 0;
@@ -912,27 +954,31 @@ __device__ void build_occurrences(const SLds<K, C> &S, uint16_t *occ, int m, int
             }
         }
     };
-    each_slot([&](int, uint32_t code) { atomicAdd(&S.cnt[code], 1u); });
+    each_slot([&](int, uint32_t code) { cnt_inc(S, code, 1u); });
     wave_sync();
     int carry = 0;
     for (int x0 = 0; x0 < 2 * (n + 1); x0 += 64) {
         const int x = x0 + ln;
-        const int cx = x < 2 * (n + 1) ? (int)S.cnt[x] : 0;
+        const int cx = x < 2 * (n + 1) ? (int)cnt_get(S, (uint32_t)x) : 0;
         const int in = wave_incl_scan(cx);
         if (x < 2 * (n + 1)) {
             S.occ_off[x] = (uint16_t)(carry + in - cx);
-            S.cnt[x] = 0u;
+            if constexpr (!cnt_packed<K, C>()) S.cnt[x] = 0u;
+            else if (!(x & 1)) S.cnt[x >> 1] = 0u;   // (both codes of the variable were read)
         }
         carry += lane63(in);
     }
     if (ln == 0) S.occ_off[2 * (n + 1)] = (uint16_t)carry;
     wave_sync();
     each_slot([&](int c, uint32_t code) {
-        const uint32_t old = atomicAdd(&S.cnt[code], 1u);
+        const uint32_t old = cnt_fetch_inc(S, code);
         occ[S.occ_off[code] + old] = (uint16_t)c;
     });
     wave_sync();
-    for (int x = ln; x < 2 * (n + 1); x += 64) S.cnt[x] = 0u;
+    if constexpr (!cnt_packed<K, C>())
+        for (int x = ln; x < 2 * (n + 1); x += 64) S.cnt[x] = 0u;
+    else
+        for (int v = ln; v <= n; v += 64) S.cnt[v] = 0u;
     // the lists are read back by this wave only: complete the stores first
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     wave_sync();
@@ -1248,7 +1294,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                 lv_clear(S.lv, (uint32_t)v);
             }
             S.ts[v] = 0u;   // (the fixed kernel's `first` flags alias ts: set by choose() before use)
-            ((uint2 *)S.cnt)[v] = make_uint2(0u, 0u);
+            cnt_clear_var(S, (uint32_t)v);
         }
     }
     if (__ballot(bad)) {
@@ -1702,7 +1748,7 @@ constexpr uint32_t FIX_LDS_BYTES = 4 * FIX_MCAP + 2 * (FIX_NCAP + 1) + 3 * 4 * (
 // up to 256 (n <= 127) or to the packing's variable limit.
 int lv_static_class(int K, int max_vars) {
     const int need = 2 * (max_vars + 1);
-    if (K == 3) return need <= 256 ? 256 : 2 * (Pack<3>::MAXV + 1);
+    if (K == 3) return need <= 256 ? 256 : need <= 512 ? 512 : 2 * (Pack<3>::MAXV + 1);
     return need <= 512 ? 512 : 2 * (Pack<5>::MAXV + 1);   // 5-SAT n <= 255: 3.5 KB less per wave
 }
 
@@ -1729,7 +1775,7 @@ bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, bool inc, u
     lay->lv = o;      o = align16(o + (with_lv ? 2 * N : 0u));   // one-wave kernel: static LDS instead
     lay->cls = o;     o = align16(o + (K == 3 ? 4u : 8u) * Mpad);
     lay->ts = o;      o = align16(o + 4 * N);
-    lay->cnt = o;     o = align16(o + 8 * N);
+    lay->cnt = o;     o = align16(o + (cb == 2 && K == 3 ? 4 : 8) * N);   // see cnt_packed
     // choose()'s flags alias the stamps when every first position + 1, (c << 3 |
     // slot) + 1, stays <= 0x10000: below any stamp of an epoch >= 1 (as in
     // dpll_fixed_kernel); larger formulas keep a separate array
@@ -1752,6 +1798,7 @@ template <bool INC>
 const void *scan_fn(int K, int lvs) {   // occupancy queries: the split form (the larger register budget)
     if (K == 3) {
         if (lvs == 256) return (const void *)dpll_scan_kernel<3, 256, INC, true>;
+        if (lvs == 512) return (const void *)dpll_scan_kernel<3, 512, INC, true>;
         if (lvs == 1024) return (const void *)dpll_scan_kernel<3, 1024, INC, true>;
         return (const void *)dpll_scan_kernel<3, 0, INC, true>;
     }
@@ -1826,6 +1873,8 @@ template <bool INC, bool SPLIT>
 void launch_kernel(int K, int lvs, dim3 g, dim3 blk, uint32_t wg_lds, hipStream_t s, const ScanArgs &A) {
     if (K == 3 && lvs == 256)
         hipLaunchKernelGGL((dpll_scan_kernel<3, 256, INC, SPLIT>), g, blk, wg_lds, s, A);
+    else if (K == 3 && lvs == 512)
+        hipLaunchKernelGGL((dpll_scan_kernel<3, 512, INC, SPLIT>), g, blk, wg_lds, s, A);
     else if (K == 3 && lvs == 1024)
         hipLaunchKernelGGL((dpll_scan_kernel<3, 1024, INC, SPLIT>), g, blk, wg_lds, s, A);
     else if (K == 3)
