@@ -64,8 +64,10 @@ def test_scan_kernel_eligibility_query():
         _capi.set_kernel(_capi.KERNEL_AUTO)
     # the launch's real per-wave LDS: one-wave workgroups keep the literal states
     # in a 256-B static array instead of the image's 2(n+1) = 202 B (+ alignment),
-    # and (n <= 127) byte-wide trail / frames / snapshot: 3 x (208 - 112) + (864 - 432)
-    assert kern == _capi.KERNEL_SCAN and s100 - 208 + 256 - 3 * 96 - 432 == lds
+    # (n <= 127) byte-wide trail / frames / snapshot: 3 x (208 - 112) + (864 - 432),
+    # and one counter word per literal code (816 B) where the 16-bit-code layout
+    # of satmi_dpll_scan_lds_bytes packs two per word (416 B)
+    assert kern == _capi.KERNEL_SCAN and s100 - 208 + 256 - 3 * 96 - 432 + (816 - 416) == lds
     # the bench class (K=3, n <= 127, m <= 448) runs the static-layout incremental
     # kernel: 5,108 B per wave whatever the instance size, 32 waves per CU
     assert lds_inc == 5108 and _capi.plan(50, 213, 639, 3)[1] == 5108
@@ -77,7 +79,10 @@ def test_scan_kernel_eligibility_query():
         lds_big_scan = _capi.plan(130, 426, 1278, 3)[1]
     finally:
         _capi.set_kernel(_capi.KERNEL_AUTO)
-    assert kern == _capi.KERNEL_INC and lds_big == lds_big_scan + 528 + 112
+    # (the incremental plan may take multi-wave workgroups when they keep more
+    # waves resident: the literal states then move from the 512-B static array
+    # into each wave's image, 2(n+1) = 262 -> 272 B)
+    assert kern == _capi.KERNEL_INC and lds_big in (lds_big_scan + 528 + 112, lds_big_scan - 512 + 272 + 528 + 112)
     _capi.set_kernel(_capi.KERNEL_GENERAL)
     try:
         assert _capi.plan(100, 426, 1278, 3)[0] == _capi.KERNEL_GENERAL
