@@ -191,7 +191,8 @@ __device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return
 // Per-literal-code counters (the counting pass, the occurrence-list build).
 // One word per code, except for 3-literal clauses with 16-bit codes (n = 128 ..
 // 511): the two codes of a variable share a word, code 2v in the low half (a
-// count is at most the clause count, <= 65,534), which halves the array --
+// count is at most the instance's literal count, which the scan kernel bounds
+// by 65,535: dpll_scan_eligible, run_queue), which halves the array --
 // uf250 fits 15 searches per CU instead of 13 (+10 %).  (5-SAT n=200 gains no
 // residency from it and pays the packing's shifts: one word per code there.)
 template <int K, typename C>
