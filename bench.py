@@ -58,7 +58,7 @@ sys.path.insert(0, os.path.join(ROOT, "sat-mpi-stana-andrei_amd"))
 import torch  # noqa: E402  (before libsatmi: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
-from satmi import _capi, cnf  # noqa: E402
+from satmi import _capi, cnf, isa  # noqa: E402
 from satmi.shard import gather_verdicts, shard_range  # noqa: E402
 
 METRIC = "instances solved/sec, random 3-SAT n=100 α=4.26; unit-props/sec; HBM GB/s"
@@ -97,7 +97,8 @@ LEGS = [
     # configs[4] solved to the end (no node limit): 512 uf250-shaped searches per
     # step, branch splitting on with helper waves on every other CU slot
     ("configs[4] uf250 solved", "uf250", ["--node-limit", "0", "--total", "512", "--split-always",
-                                          "--helpers-per-cu", "10", "--steps", "2", "--warmup", "0"]),
+                                          "--helpers-per-cu", "10", "--steps", "2", "--warmup", "0",
+                                          "--cpu-scaled"]),
     ("cdcl", "cdcl", ["--steps", "3", "--warmup", "1"]),
     ("cdcl 4 threads", "cdcl", ["--steps", "3", "--warmup", "1", "--threads", "4"]),
 ]
@@ -123,8 +124,17 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=20251016)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-scaled", action="store_true",
+                   help="searches too long for any bounded CPU sample (uf250 solved to the end): the CPU sample is "
+                        "node-capped at --cpu-sample-node-limit and its unit-props/s scaled to instances/s by the "
+                        "GPU's unit propagations per instance (default: the oracle solves whole instances)")
     p.add_argument("--cpu-sample-node-limit", type=int, default=2000,
-                   help="searches solved to the end: the CPU sample's node cap (its rate scaled to instances/s)")
+                   help="--cpu-scaled: the CPU sample's node cap")
+    p.add_argument("--emulate-world", type=int, default=0,
+                   help="on one GPU, run exactly rank --emulate-rank's shard of an N-rank job (the 8-GPU imbalance)")
+    p.add_argument("--emulate-rank", type=int, default=0)
+    p.add_argument("--full-json", default=None,
+                   help="also write the uncompacted line (every leg's full objects) to this file")
     p.add_argument("--no-legs", action="store_true", help="only the headline workload (no `configs` object)")
     p.add_argument("--legs-only", action="store_true", help=argparse.SUPPRESS)   # the child of the default run
     p.add_argument("--legs-hwq17", action="store_true", help=argparse.SUPPRESS)  # ... its HWQ17_LEGS child
@@ -257,10 +267,11 @@ def load_profile(name, key):
         return None
 
 
-def kernel_src_sha(kernel="dpll"):
-    src = {"dpll": "dpll_scan.hip", "cdcl": "cdcl.hip", "res": "resolution.hip", "dp": "dp.hip"}[kernel]
-    with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", src), "rb") as fh:
-        return hashlib.sha256(fh.read()).hexdigest()[:16]
+def kernel_isa_sha(base):
+    """16 hex digits of the machine code of the kernels named `base` in the
+    loaded libsatmi.so (satmi/isa.py): the identity an SQ profile entry is
+    keyed on, so a comment-only source edit does not make it stale."""
+    return isa.kernel_code_sha(base)
 
 
 def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll", clock_hz=None):
@@ -269,7 +280,8 @@ def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll", clock_hz=None):
     wave-instructions / LDS-array cycles per launch of this exact workload) over
     this run's live kernel time at the peak engine clock.  Peaks: VALU 0.5
     wave-instructions / cycle / SIMD, SALU 1 / cycle / CU, LDS array 1 cycle /
-    cycle / CU.  `stale` if the kernel source changed since the profile."""
+    cycle / CU.  `stale` if the kernel's machine code in the loaded library differs from
+    the code the profile was taken on (entry `kernel_isa_sha16`)."""
     e = load_profile("sq_issue.json", f"{preset}_B{per_gpu}")
     if not e:
         return None
@@ -293,7 +305,7 @@ def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll", clock_hz=None):
             "clock_hz": hz, "clock_source": "live (in-kernel s_memtime / s_memrealtime)" if clock_hz else "peak",
             "profile_clock_hz": e["effective_clock_hz"], "source": e["source"],
             "kernel": e.get("kernel"),
-            "stale": e["kernel_src_sha256_16"] != kernel_src_sha(kernel)}
+            "stale": e.get("kernel_isa_sha16") != kernel_isa_sha(e.get("kernel", kernel).split("<")[0])}
 
 
 def dpll_kernel_name(n, m, k, split):
@@ -363,7 +375,10 @@ def run_dpll(args, world, rank, local):
     _capi.set_split_warmup(args.split_warmup)
 
     n, k = args.n, args.k
-    b0, b1 = shard_range(args.total, world, rank)   # this rank's contiguous shard of the step's batch
+    # this rank's contiguous shard of the step's batch (--emulate-world: the
+    # shard rank r of an N-rank job would get, run alone on this GPU)
+    sw, sr = (args.emulate_world, args.emulate_rank) if args.emulate_world else (world, rank)
+    b0, b1 = shard_range(args.total, sw, sr)
     B = b1 - b0
     m = int(round(args.alpha * n))
     # NS distinct resident batches, rotated step to step (batch j: the virtual
@@ -477,7 +492,7 @@ def run_dpll(args, world, rank, local):
     # the last step's per-instance verdicts gathered over the process group
     # (RCCL all-gather): the same hash for every rank count
     sat_last = (counters[:, 5] > 0).to(torch.int8)
-    verdicts, ctr_tot = gather_verdicts(sat_last, counters, args.total, device=dev)
+    verdicts, ctr_tot = gather_verdicts(sat_last, counters, B if args.emulate_world else args.total, device=dev)
     seen = torch.ones(1, dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(seen)
@@ -532,7 +547,9 @@ def run_dpll(args, world, rank, local):
                    "parallelism": f"instance-sharded x{world}", "streams": NS,
                    "branch_splitting": not args.no_split,
                    "split_policy": "off" if args.no_split else "always" if args.split_always else "auto",
-                   "helpers_per_cu": args.helpers_per_cu or 1, "split_warmup": args.split_warmup},
+                   "helpers_per_cu": args.helpers_per_cu or 1, "split_warmup": args.split_warmup,
+                   "emulated_shard": ({"world": sw, "rank": sr, "begin": b0, "end": b1} if args.emulate_world
+                                      else None)},
         "instances_per_s": all_inst / elapsed,
         "unit_props_per_s": props / elapsed,
         "capped_fraction": int(((status == 2).sum()).item()) / B,
@@ -881,7 +898,8 @@ def run_one(args, world, rank, local):
         return run_cdcl(args, world, rank, local)
     out, host = run_dpll(args, world, rank, local)
     ppi = out["unit_props_per_s"] / out["instances_per_s"] if out["instances_per_s"] else None
-    out["cpu_baseline"] = (cpu_baseline(host, args.cpu_seconds, args.node_limit, ppi, args.cpu_sample_node_limit)
+    scaled = args.cpu_sample_node_limit if args.cpu_scaled else 0
+    out["cpu_baseline"] = (cpu_baseline(host, args.cpu_seconds, args.node_limit, ppi, scaled)
                            if host is not None else None)
     return out
 
@@ -898,14 +916,74 @@ def legs_main(args):
         a = parse(["--workload", wl, "--cpu-seconds", str(args.leg_cpu_seconds), "--seed", str(args.seed)] + extra)
         t = time.perf_counter()
         r = run_one(a, 1, 0, 0)
-        keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_issue",
-                "cpu_baseline", "result", "passes_or_steps", "instances_per_s", "unit_props_per_s",
-                "capped_fraction", "sat_fraction", "sat", "unsat", "iteration_capped", "iterations_per_s",
-                "verdict_sha", "kernel_ms", "wave_utilisation", "oracle_check", "resident_waves", "branch_split",
-                "derived_clauses_per_s")
-        out[name] = {k: r[k] for k in keep if k in r}
-        out[name]["leg_wall_s"] = time.perf_counter() - t
+        r["leg_wall_s"] = time.perf_counter() - t
+        out[name] = r
     print(json.dumps(out), flush=True)
+
+
+# The printed line stays well inside what the driver parses (r05's 25 KB line
+# was not parsed; r04's 17.5 KB was): the headline keeps its full roofline,
+# issue roofline and CPU baseline, each leg only its figures.  --full-json
+# writes the uncompacted line beside it.
+LINE_BUDGET = 8000
+HEAD_ROOF = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms", "kernel_ms_hip_events",
+             "kernel_ms_exclusive", "frac_exclusive", "algorithmic_bytes_per_launch")
+HEAD_ISSUE = ("bound", "achieved", "peak", "unit", "frac", "fracs", "lds_bank_conflict_share", "clock_source",
+              "kernel", "source", "stale")
+HEAD_CPU = ("value", "unit", "cores", "kind", "sample")
+HEAD_DROP = ("configs", "configs_note", "branch_split", "roofline", "roofline_issue", "cpu_baseline")
+
+
+def _sig(x, digits=4):
+    """Floats to `digits` significant digits, recursively (the line's size)."""
+    if isinstance(x, float):
+        return float(f"{x:.{digits}g}")
+    if isinstance(x, dict):
+        return {k: _sig(v, digits) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_sig(v, digits) for v in x]
+    return x
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if d and k in d} if d else None
+
+
+def compact_leg(r):
+    """A secondary config's figures: value, unit, time per step, the binding
+    roofline fractions, the CPU baseline and the verdict hash."""
+    out = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps") if k in r}
+    roof, iss, cpu = r.get("roofline"), r.get("roofline_issue"), r.get("cpu_baseline")
+    out["roofline"] = _pick(roof, ("bound", "frac"))
+    if iss:
+        out["roofline_issue"] = _pick(iss, ("bound", "frac", "stale"))
+    out["cpu_baseline"] = _pick(cpu, ("value", "unit", "cores"))
+    for k in ("verdict_sha", "capped_fraction", "wave_utilisation"):
+        if k in r:
+            out[k] = r[k]
+    return _sig(out)
+
+
+def compact_line(full):
+    """The printed line: every contract key and the headline's figures in full,
+    its roofline / issue roofline / CPU baseline trimmed to their figures, the
+    legs compacted (compact_leg)."""
+    out = {k: v for k, v in full.items() if k not in HEAD_DROP}
+    out["roofline"] = _sig(_pick(full.get("roofline"), HEAD_ROOF))
+    if full.get("roofline_issue") is not None:
+        out["roofline_issue"] = _sig(_pick(full["roofline_issue"], HEAD_ISSUE))
+    cpu = full.get("cpu_baseline")
+    if cpu is not None:
+        c = _pick(cpu, HEAD_CPU)
+        if isinstance(cpu.get("single_core"), dict):
+            c["single_core_value"] = cpu["single_core"].get("instances_per_s")
+        out["cpu_baseline"] = _sig(c)
+    bs = full.get("branch_split")
+    if bs:
+        out["branch_split"] = {k: bs[k] for k in ("donations", "helpers", "done") if k in bs}
+    if "configs" in full:
+        out["configs"] = {name: compact_leg(r) for name, r in full["configs"].items()}
+    return out
 
 
 def main():
@@ -913,12 +991,14 @@ def main():
     if args.legs_only:
         return legs_main(args)
     world, rank, local = init_ranks()
+    if args.emulate_world and (world > 1 or not 0 <= args.emulate_rank < args.emulate_world):
+        raise SystemExit("bench: --emulate-world runs one rank's shard in a 1-process job (0 <= rank < world)")
     if args.workload == "3sat-n50" and (args.streams or 16) > 3 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 17:
         print("bench: note: GPU_MAX_HW_QUEUES < streams + 1, the streams share hardware queues", file=sys.stderr)
     t_start = time.perf_counter()
     out = run_one(args, world, rank, local)
     legs = (world == 1 and not args.no_legs and not args.profile_steps and args.workload == "3sat-n100"
-            and args.total == WORKLOADS["3sat-n100"][0])
+            and args.total == WORKLOADS["3sat-n100"][0] and not args.emulate_world)
     if legs and rank == 0:
         got = {}
         for hwq in (False, True):
@@ -931,18 +1011,14 @@ def main():
             if r.returncode != 0:
                 raise SystemExit(f"bench: secondary configs failed:\n{r.stderr[-4000:]}")
             got.update(json.loads(r.stdout.strip().splitlines()[-1]))
+        # (DESIGN.md "Measurement": how the legs run and which answers configs[1])
         out["configs"] = {name: got[name] for name, _, _ in LEGS if name in got}
-        out["configs_note"] = ("the other BASELINE configs, measured after the headline by two child processes "
-                               "(bench.py --legs-only; the 16-stream leg with GPU_MAX_HW_QUEUES=17, the rest with "
-                               "HIP's default queues) with the same harness; "
-                               "configs[1] ('4,096 instances, n=50, on 1 MI355X') is answered by the 2-stream "
-                               "leg: batches of 4,096 solved back to back, the next batch's waves taking the CUs "
-                               "the current batch's tail leaves idle (at most 8,192 instances resident); the "
-                               "16-stream leg (16 batches resident, ~65 k instances in flight) is a saturation "
-                               "ceiling for a stream of such batches, not the configs[1] figure")
     if rank == 0:
         out["wall_s"] = time.perf_counter() - t_start
-        print(json.dumps(out), flush=True)
+        if args.full_json:
+            with open(args.full_json, "w") as fh:
+                json.dump(out, fh)
+        print(json.dumps(compact_line(out)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

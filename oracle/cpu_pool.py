@@ -68,10 +68,15 @@ def _worker(args):
     oracle.lib()
     t0 = time.perf_counter()
     done = props = 0
+    if B <= 0:
+        return done, props, time.perf_counter() - t0
     replicas = kind in ("dp", "res")
     cycle = kind in ("resset", "dpset")
     f0 = _instance(icb, clb, lits, 0) if replicas else None
-    b = w % B
+    # the sample's instances are solved once each, except by the cycling kinds:
+    # a worker past the sample's end has nothing to do (it must not solve and
+    # count an instance another worker already counted)
+    b = w % B if cycle else w
     while replicas or cycle or b < B:
         u, p = _solve(kind, f0 if replicas else _instance(icb, clb, lits, b), param)
         done += u

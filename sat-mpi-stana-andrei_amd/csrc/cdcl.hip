@@ -359,6 +359,9 @@ __device__ __forceinline__ bool lit_false(const St &S, int lit) {
 #ifndef CDCL_WCH
 #define CDCL_WCH 4          // 64-slot chunks per propagate window (reads in flight)
 #endif
+// own8 holds one window of 64 * 4 slots (cleared as 64 words) and the conflict
+// scan's "none" sentinel is chunk 4: a wider window would overrun both
+static_assert(CDCL_WCH >= 1 && CDCL_WCH <= 4, "CDCL_WCH: 1..4 chunks per propagate window");
 
 __device__ int64_t propagate(const CdclArgs &A, const St &S, Seq &q) {
     __shared__ __attribute__((aligned(4))) uint8_t own8[256];   // window slot -> owning key lane (one-wave groups)

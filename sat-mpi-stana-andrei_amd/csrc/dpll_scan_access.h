@@ -71,11 +71,13 @@ __device__ __forceinline__ void dup_assign_store(const SLds<K, C> &S, bool first
 #endif
 }
 
-// the counting pass's duplicated atomic (attribution only)
+// the counting pass's duplicated atomic (attribution only), at the address
+// cnt_inc uses: with packed counters (K = 3, 16-bit codes) a variable's two
+// codes share the word cnt[code >> 1]
 template <int K, typename C>
 __device__ __forceinline__ void dup_count(const SLds<K, C> &S, uint32_t code) {
 #ifdef SATMI_DUP_CNT
-    atomicAdd(&S.cnt[code], opaque_zero());
+    atomicAdd(&S.cnt[(sizeof(C) == 2 && K == 3) ? (code >> 1) : code], opaque_zero());
 #else
     (void)S;
     (void)code;

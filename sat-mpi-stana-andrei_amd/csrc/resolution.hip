@@ -623,11 +623,12 @@ __device__ void finish_pass(const ResArgs &A, ResState *S, int64_t nnew, int64_t
 // finishes last sums the claims over the stripes, takes the verdict or sets
 // the next pass's bounds and resets the counters -- one launch per pass
 // instead of a gather and a one-workgroup finish kernel (each launch boundary
-// was ~4.6 us of a php-res call).  The last block needs nothing the other
-// blocks wrote in this launch (the counts are the pass kernel's atomics, the
-// overflow conditions it derives itself), so the count of finished blocks is
-// a relaxed atomic with no release / acquire fences; every block has read the
-// stripes and the state before its count, so the last block may rewrite them.
+// was ~4.6 us of a php-res call).  The last block needs nothing else the
+// other blocks wrote in this launch (the counts are the pass kernel's
+// atomics, the overflow conditions it derives itself) except block (0,0)'s
+// S->tk_last, so only that block's count is a release (and the last block
+// fences); every block has read the stripes and the state before its count,
+// so the last block may rewrite them.
 __global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
     __shared__ int64_t pre[RES_STRIPES + 1];
     __shared__ int64_t cnt[RES_STRIPES], cand[RES_STRIPES];
@@ -662,11 +663,19 @@ __global__ void __launch_bounds__(256) res_gather_kernel(ResArgs A) {
     __syncthreads();
     if (tid == 0) {
         const unsigned long long nb = (unsigned long long)gridDim.x * gridDim.y;
-        sh_last = __hip_atomic_fetch_add(A.stripes + RES_GDONE, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                  nb - 1;
+        // block (0,0) wrote S->tk_last in this launch: its count is a release
+        // (the other blocks' stay relaxed and continue its release sequence),
+        // and the last block takes an acquire fence below before finish_pass
+        // reads it
+        const bool b00 = blockIdx.x == 0 && blockIdx.y == 0;
+        const unsigned long long prev =
+            b00 ? __hip_atomic_fetch_add(A.stripes + RES_GDONE, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
+                : __hip_atomic_fetch_add(A.stripes + RES_GDONE, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh_last = prev == nb - 1;
     }
     __syncthreads();
     if (!sh_last) return;
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (tid < RES_STRIPES) {
         cnt[tid] = (int64_t)(A.stripes[tid] - (unsigned long long)A.slot_base);
         cand[tid] = (int64_t)A.stripes[RES_STRIPES + tid];
@@ -1311,6 +1320,10 @@ extern "C" int satmi_resolution_host(int nclauses, const int32_t *h_clause_off, 
     }
     DevBuf &table = wk->table, &flag = wk->flag, &pos = wk->pos, &slotv = wk->slotv, &tiles = wk->tiles,
            &grand = wk->grand;
+    // the general path fills the shared table with clause indices: a later
+    // packed call on this workspace must empty it first (its prologue only
+    // skips the reset when the previous packed call's reset left it clean)
+    wk->clean = ResWork::Clean{};
     EventTimer &t_pairs = wk->t_pairs, &t_claims = wk->t_claims;
     t_pairs.reset();
     t_claims.reset();

@@ -58,3 +58,28 @@ def test_saturation_roofline_prices_the_pipes_at_the_live_clock():
     for k, v in r["fracs"].items():
         assert abs(v * 1.3e9 / bench.PEAK_CLOCK_HZ - peak["fracs"][k]) < 1e-12
         assert abs(r["fracs_at_peak_clock"][k] - peak["fracs"][k]) < 1e-12
+
+
+def test_issue_roofline_staleness_follows_the_machine_code(monkeypatch):
+    """`stale` compares the entry's kernel_isa_sha16 with the machine code of
+    the kernel in the loaded library (satmi/isa.py), not the source text."""
+    e = bench.load_profile("sq_issue.json", "php-res_B1")
+    monkeypatch.setattr(bench, "kernel_isa_sha", lambda base: e["kernel_isa_sha16"])
+    assert bench.issue_roofline("php-res", 1, 0.25, kernel="res")["stale"] is False
+    monkeypatch.setattr(bench, "kernel_isa_sha", lambda base: "0" * 16)
+    assert bench.issue_roofline("php-res", 1, 0.25, kernel="res")["stale"] is True
+
+
+def test_every_profiled_kernel_is_found_in_the_library():
+    import json
+    import os
+    import pytest
+    from satmi import _capi, isa
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("libsatmi.so not built")
+    with open(os.path.join(os.path.dirname(bench.__file__), "profiles", "sq_issue.json")) as fh:
+        table = json.load(fh)
+    for key, e in table.items():
+        sha = isa.kernel_code_sha(e["kernel"].split("<")[0])
+        assert sha is not None and len(sha) == 16, key
+        assert e.get("kernel_isa_sha16") and len(e["kernel_isa_sha16"]) == 16, key

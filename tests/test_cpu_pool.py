@@ -34,3 +34,17 @@ def test_dpll_kind_walks_the_sample_once(tmp_path):
     r = cpu_pool.run("dpll", _save(tmp_path, batch), 30.0, 0, 2)
     assert r["units"] == 5
     assert r["unit_props"] > 0
+
+
+def test_dpll_kind_with_more_workers_than_instances(tmp_path):
+    """a worker past the sample's end solves nothing (it must not
+    solve and count an instance another worker counted); an empty sample is
+    no error."""
+    batch = cnf.uniform_ksat(2, 10, 42, 3, seed=9)
+    r = cpu_pool.run("dpll", _save(tmp_path, batch), 30.0, 0, 5)
+    assert r["units"] == 2
+    empty = tmp_path / "empty"
+    empty.mkdir()
+    for name, arr in (("icb", [0]), ("clb", [0]), ("lits", [0])):
+        np.save(os.path.join(empty, name + ".npy"), np.asarray(arr, dtype=np.int32))
+    assert cpu_pool.run("dpll", str(empty), 1.0, 0, 2)["units"] == 0

@@ -235,3 +235,33 @@ def test_bench_random_unsat_set_matches_oracle():
         assert r["result"] == o["result"]
         assert list(r["pass_new"]) == list(o["pass_new"])
         assert [sorted(p) for p in r["clauses"]] == [sorted(p) for p in o["clauses"]]
+
+
+def test_general_then_packed_calls_share_the_table():
+    """the general path (> 31 variables) fills the workspace's
+    table with clause indices; the next packed call (<= 31 variables) on the
+    same thread reuses that table and must empty it first.  A stale index i
+    equals the packed key of the all-positive clause over dense variables
+    bit-set i, so the packed formulas here are full of small all-positive
+    clauses; every call's passes must equal the oracle's."""
+    from satmi import _capi
+    rng = random.Random(71)
+    nvars = 40
+    vs = list(range(1, nvars + 1))
+    big = [[v if rng.random() < 0.5 else -v for v in vs[i:i + 3]] for i in range(0, nvars, 3)]
+    big += [[v if rng.random() < 0.5 else -v for v in rng.sample(vs, 2)] for _ in range(30)]
+    small = [
+        [[1, 2], [1], [2], [1, 3], [-1, -2, 3], [-3, 4], [-4]],
+        [[1, 2], [2, 3], [1, 3], [-1, -2], [-2, -3], [-1, -3], [1, 2, 3]],
+        [[1], [2], [1, 2], [3], [1, 3], [2, 3], [1, 2, 3], [-1, -2, -3]],
+    ]
+    want_big = oracle.resolution(big, record=True, max_passes=2)
+    want = [oracle.resolution(f, record=True) for f in small]
+    _capi.trim_workspaces()
+    for k in range(6):
+        f, w = small[k % 3], want[k % 3]
+        r = resolve(f, record=True)
+        assert (r["result"], r["pass_new"]) == (w["result"], w["pass_new"]), (k, f)
+        assert [sorted(p) for p in r["clauses"]] == [sorted(p) for p in w["clauses"]], (k, f)
+        rb = resolve(big, record=True, max_passes=2)
+        assert (rb["result"], rb["pass_new"]) == (want_big["result"], want_big["pass_new"]), k

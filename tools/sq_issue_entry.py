@@ -14,7 +14,8 @@ bank-conflict cycles beside it), and the effective clock = GRBM_GUI_ACTIVE per
 XCD / the live launch time the profiled bench line reports (`kernel_ms`).
 bench.py divides the counts by the live kernel time and the pipe peaks (VALU
 0.5 wave-instr / cycle / SIMD, SALU 1 / cycle / CU, LDS 1 array cycle / cycle /
-CU); the entry carries the kernel source hash (stale when the source changes).
+CU); the entry carries the kernel's machine-code hash (satmi/isa.py: stale when the
+code object changes, not on comment edits) and, for reference, the source hash.
 """
 import hashlib
 import json
@@ -57,8 +58,14 @@ def main():
     cyc = clock * kms * 1e-3
     with open(os.path.join(ROOT, "sat-mpi-stana-andrei_amd", "csrc", ksrc), "rb") as fh:
         sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    # the staleness key: the kernel's machine code in the in-tree libsatmi.so
+    # (the library the profiled run shipped with -- enter the profile before
+    # rebuilding)
+    sys.path.insert(0, os.path.join(ROOT, "sat-mpi-stana-andrei_amd"))
+    from satmi import isa
+    isa_sha = isa.kernel_code_sha(kname.split("<")[0])
     entry = {
-        "kernel": kname, "kernel_src_sha256_16": sha, "dispatches": nd, "profiled_kernel_ms": kms,
+        "kernel": kname, "kernel_src_sha256_16": sha, "kernel_isa_sha16": isa_sha, "dispatches": nd, "profiled_kernel_ms": kms,
         "per": "step" if per_step else "launch",
         "effective_clock_hz": clock,
         "valu_insts": per("SQ_INSTS_VALU"), "salu_insts": per("SQ_INSTS_SALU"), "lds_insts": per("SQ_INSTS_LDS"),
