@@ -25,7 +25,10 @@ child process after the headline -- the line's `configs` object):
     uf250      configs[4]: uf250-1065 shape (random 3-SAT n=250, m=1065),
                node-capped search (--node-limit, default 20,000 calls/instance)
     5sat-n200  configs[4]: random 5-SAT n=200 at the 5-SAT threshold
-               (alpha=21.117, m=4,223): long clauses, 4 waves per CU of LDS
+               (alpha=21.117, m=4,223): long clauses, 4 waves per CU of LDS,
+               node-capped search (--node-limit, default 20,000)
+    5sat-n200-a12  configs[4]: random 5-SAT n=200 at alpha 12 (m=2,400), every
+               search decided to the end (no node limit) -- instances/s
     php-dp     configs[3]: Davis-Putnam elimination of pigeonhole PHP(6,5)
                (30 variables, 81 clauses; every step's resolvents, tautology
                and subsumption filter on the GPU) -- solves/s
@@ -74,6 +77,10 @@ WORKLOADS = {
     "3sat-n50": (4096, 50, 4.26, 3, 0, "configs[1]"),
     "uf250": (7680, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,840 resident waves (15 / CU)
     "5sat-n200": (2048, 200, 21.117, 5, 20000, "configs[4]"),  # 2 x the 1,024 resident waves (4 / CU)
+    # configs[4]'s 5-SAT n=200 decided to the end: alpha 12 (m=2,400), where
+    # every search of a batch finishes (at the threshold none of 64 did in 90 s:
+    # profiles/r06/fullsolve_5sat_probe.txt)
+    "5sat-n200-a12": (2048, 200, 12.0, 5, 0, "configs[4]"),
 }
 # configs[3] presets: (holes, resolution passes) -- one formula per step, host-array C ABI
 SATURATION = {"php-dp": (5, 0), "php-res": (3, 4)}
@@ -99,6 +106,9 @@ LEGS = [
     ("configs[4] uf250 solved", "uf250", ["--node-limit", "0", "--total", "512", "--split-always",
                                           "--helpers-per-cu", "10", "--steps", "2", "--warmup", "0",
                                           "--cpu-scaled"]),
+    # 5-SAT n=200 decided to the end (alpha 12), split always
+    ("configs[4] 5sat-n200 solved", "5sat-n200-a12", ["--split-always", "--steps", "2", "--warmup", "1",
+                                                     "--cpu-scaled"]),
     ("cdcl", "cdcl", ["--steps", "3", "--warmup", "1"]),
     ("cdcl 4 threads", "cdcl", ["--steps", "3", "--warmup", "1", "--threads", "4"]),
 ]
@@ -144,7 +154,7 @@ def parse(argv=None):
                    help="DPLL kernel policy (satmi_dpll_set_kernel); auto = incremental clause kernel")
     p.add_argument("--no-split", action="store_true", help="disable branch splitting (satmi_dpll_set_split)")
     p.add_argument("--split-always", action="store_true",
-                   help="split every eligible launch (default: at least 1 and fewer than 4 instances per resident wave)")
+                   help="split every eligible launch (default: at least 1 and at most 8 instances per resident wave)")
     p.add_argument("--split-warmup", type=int, default=-1,
                    help="nodes before a search may donate (satmi_dpll_set_split_warmup; -1 = default)")
     p.add_argument("--helpers-per-cu", type=int, default=0, help="branch-splitting helpers per CU (0 = library default)")
@@ -305,7 +315,7 @@ def issue_roofline(preset, per_gpu, kernel_ms, kernel="dpll", clock_hz=None):
             "clock_hz": hz, "clock_source": "live (in-kernel s_memtime / s_memrealtime)" if clock_hz else "peak",
             "profile_clock_hz": e["effective_clock_hz"], "source": e["source"],
             "kernel": e.get("kernel"),
-            "stale": e.get("kernel_isa_sha16") != kernel_isa_sha(e.get("kernel", kernel).split("<")[0])}
+            "stale": e.get("kernel_isa_sha16") != kernel_isa_sha(e.get("isa_symbol") or e["kernel"].split("<")[0])}
 
 
 def dpll_kernel_name(n, m, k, split):
@@ -515,8 +525,10 @@ def run_dpll(args, world, rank, local):
     # (csrc/dpll_scan.hip dpll_scan_launch): they count as resident
     extra = ncu * (args.helpers_per_cu or 1) if split_used else 0
     resident = min(B + extra, ncu * per_cu)
+    # NS streams' launches overlap: at most every CU slot busy at once
+    resident_all = min(NS * (B + extra), ncu * per_cu)
     # busy wave-time over resident wave-time of the timed region (all streams)
-    util = ticks / world / hz / (resident * elapsed)
+    util = ticks / world / hz / (resident_all * elapsed)
     pmc = load_profile("pmc_traffic.json", workload)
     kname = dpll_kernel_name(n, m, k, split_used)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -980,7 +992,7 @@ def compact_line(full):
         out["cpu_baseline"] = _sig(c)
     bs = full.get("branch_split")
     if bs:
-        out["branch_split"] = {k: bs[k] for k in ("donations", "helpers", "done") if k in bs}
+        out["branch_split"] = dict(bs)
     if "configs" in full:
         out["configs"] = {name: compact_leg(r) for name, r in full["configs"].items()}
     return out

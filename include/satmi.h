@@ -272,7 +272,7 @@ int satmi_dpll_set_kernel(int policy);
  * cancelled and count nothing).  Applies to SOUND-mode launches with
  * max_solutions == 1, no node limit and no time limit.
  *   enable          0 off; 1 auto (default): launches with at least one and
- *                   fewer than 4 instances per resident wavefront; 2 every
+ *                   at most 8 instances per resident wavefront; 2 every
  *                   eligible launch
  *   helpers_per_cu  wavefronts per CU that stay as helpers once the queue
  *                   drains (0 = default 1); the others exit, freeing their CU
@@ -288,7 +288,9 @@ int satmi_dpll_set_split_warmup(int nodes);
 /* Branch-splitting statistics of the last DPLL launch on `stream` (waits for
  * the stream): out[0..6] = donations, helper tickets, subtrees run by helpers,
  * donations taken back by their donors, waves that registered as helpers,
- * donors' ticks spent waiting on helpers, root instances finished.  All zero
+ * searches handed to a helper (a donor that reaches a branch its helper is
+ * still searching passes it the rest of its search instead of waiting; until
+ * r06 this entry was the donors' waiting ticks), root instances finished.  All zero
  * (out[6] = 0) when that launch did not split. */
 int satmi_dpll_split_stats(void *stream, int64_t *out);
 

@@ -35,7 +35,7 @@ struct ScanLaunch {
     // `stream` and the launch's tag for the slot states (distinct per launch on
     // the stream), nullptr on failure
     bool split = false;
-    bool split_always = false;   // split any eligible launch (else only 1 <= instances per resident wave < 8)
+    bool split_always = false;   // split any eligible launch (else only 1 <= instances per resident wave <= 8)
     int split_helpers_per_cu = SPLIT_HELPERS_PER_CU;   // waves per CU that stay as helpers once the queue drains
     int split_warmup = SPLIT_WARMUP_NODES;   // nodes of a search before its first donation
     std::function<void *(size_t, uint32_t *)> split_alloc;
@@ -52,7 +52,7 @@ int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, bool i
                        uint32_t *lds_per_wave = nullptr);
 
 // Bytes of the splitting scratch head, and its statistics decoded from a host
-// copy of it: [donations, tickets, claims, reclaims, helpers, wait_ticks, done].
+// copy of it: [donations, tickets, claims, reclaims, helpers, handoffs, done].
 constexpr int SPLIT_HEAD_BYTES = 512;
 void dpll_split_decode(const void *head, int64_t out[7]);
 

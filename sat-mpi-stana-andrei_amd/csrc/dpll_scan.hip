@@ -1046,6 +1046,20 @@ __device__ uint64_t flush_counters(int64_t *ctr, Ctr32 &c, bool &flushed) {
 // So the split search reports exactly the sequential one.  Used only where
 // that holds: SOUND mode, stop at the first model, no node or time limit.
 //
+// Hand-off instead of a wait (r06): a donor whose backtracking reaches a
+// donated frame that a helper is still searching does not wait for it.  It
+// writes the rest of its search -- its identity (root instance or task slot),
+// its decision frames above the donated one and its live donation stack --
+// into the slot as a continuation, marks the slot HANDED, and is free for
+// other work.  The helper, on finishing the subtree, finds its slot HANDED
+// instead of publishing it, and continues the donor's search itself in its own
+// LDS: same instance (clauses and occurrence lists already staged), same trail
+// prefix (the subtree started from the donor's trail before the donated
+// decision), the donor's frames and donation stack restored, its result taken
+// exactly as the donor would have taken it (UNSAT: backtracking goes on; SAT:
+// the model is the search's).  No wave ever waits on another, so a search split
+// many ways no longer leaves donors idle on chains of joins.
+//
 // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): payload written
 // through (agent atomic stores), `s_waitcnt vmcnt(0)`, then the state flag by
 // an agent atomic; the reader polls the flag relaxed, then one agent acquire
@@ -1064,14 +1078,16 @@ struct SplitCfg {
     uint32_t done;             // line 2: root instances finished
     int32_t helpers;           //         waves that registered as helpers
     uint32_t claims, reclaims; //         statistics: subtrees run by helpers, taken back by donors
-    unsigned long long wait_ticks;   //   donors' time waiting on helpers
+    unsigned long long handoffs;     //   continuations handed to helpers (see "Hand-off")
     uint32_t pad2[26];
     int32_t slot_cap, slot_bytes, dstack_cap;   // line 3: geometry (read only)
     uint32_t epoch;            // launch tag of the slot states (the pool is not cleared between launches)
     int32_t max_helpers;       // waves beyond this count exit when the queue drains (their CU slots go
                                // to the next launch on another stream)
     uint32_t warm;             // nodes of a search before it may donate
-    uint32_t pad3[26];
+    int32_t cont_off;          // slot offset of the continuation: frames fvar[], ftrail[] (cont_fb bytes
+    int32_t cont_fb;           // each), then the donation stack (int32)
+    uint32_t pad3[24];
 };
 constexpr int SPLIT_POOL_OFF = 512;
 static_assert(sizeof(SplitCfg) == SPLIT_POOL_OFF, "SplitCfg layout");
@@ -1079,23 +1095,32 @@ static_assert(sizeof(SplitCfg) == SPLIT_POOL_OFF, "SplitCfg layout");
 // existing event test (next_event), so the split form's loop carries no
 // per-decision counter: what it keeps live is only read at the checks.
 constexpr uint32_t SPLIT_CHECK_NODES = 16u;
-constexpr int SPLIT_MAX_PER_WAVE = 4;   // split a launch only below this many instances per resident wave (r05 sweep: profiles/r05/n8share.json)
+constexpr int SPLIT_MAX_PER_WAVE = 8;   // split a launch only up to this many instances per resident wave (r06: every
+                                         // rank's shard at N=8 / 4 / 2, profiles/r06/slices.json)
 // Kernels come in two forms: SPLIT = false has no branch-splitting code at all
 // (its register cost -- SGPR spills in the node loop -- was measured at ~4 % of
 // the full-size rate), SPLIT = true can split.  The host launches the split
 // form only for launches with few instances per resident wave.
-enum : uint32_t { SL_PENDING = 1, SL_RUNNING = 2, SL_DONE = 3, SL_RECLAIMED = 4 };
+enum : uint32_t { SL_PENDING = 1, SL_RUNNING = 2, SL_DONE = 3, SL_RECLAIMED = 4, SL_HANDED = 5 };
 struct SlotFlags {     // line 0 of a slot
     uint32_t state;    // split_epoch << 4 | SL_*
     uint32_t cancel;   // the donor no longer needs the result
 };
 struct SlotHdr {       // line 1 (payload)
-    int32_t inst, tl0, dec_code, status, model_len, pad[3];
+    int32_t inst, tl0, dec_code, status, model_len;
+    int32_t cont_task, cont_depth, cont_nd;   // a handed-over continuation: identity (-1: the root
+                                              // search of `inst`), its frames and live donations
     int64_t ctr[SATMI_NCOUNTERS];
 };
 constexpr int SLOT_HDR_OFF = 128, SLOT_TRAIL_OFF = 256;
+// a slot: flags line, payload line, the trail (prefix in, model out), then the
+// continuation area (frames fvar / ftrail, the donation stack)
+__host__ __device__ __forceinline__ int slot_frames_bytes(int ncap, int cb) { return ((ncap + 1) * cb + 127) & ~127; }
+__host__ __device__ __forceinline__ int slot_cont_off(int ncap, int cb) {
+    return SLOT_TRAIL_OFF + slot_frames_bytes(ncap, cb);
+}
 __host__ __device__ __forceinline__ int slot_bytes_for(int ncap, int cb) {
-    return SLOT_TRAIL_OFF + (((ncap + 1) * cb + 127) & ~127);
+    return slot_cont_off(ncap, cb) + 2 * slot_frames_bytes(ncap, cb) + ((4 * (ncap + 1) + 127) & ~127);
 }
 
 struct SlotRef {
@@ -1203,33 +1228,54 @@ __device__ void cancel_donations(const ScanArgs &A, const int32_t *dst, int nd) 
     }
 }
 
-enum { TAKE_LOCAL = 0, TAKE_UNSAT = 1, TAKE_SAT = 2, TAKE_CANCELLED = 3 };
+enum { TAKE_LOCAL = 0, TAKE_UNSAT = 1, TAKE_SAT = 2, TAKE_CANCELLED = 3, TAKE_HANDED = 4 };
 
-// The donor's backtracking reached donated slot s: reclaim it if no helper
-// took it (TAKE_LOCAL: search the branch here), else wait for the helper's
-// result (its payload readable after the acquire).  A task that is itself
-// cancelled while waiting passes the cancellation on and returns TAKE_CANCELLED.
-__device__ int take_donation(const ScanArgs &A, int s, const SlotFlags *mine, int64_t *ctr) {
+// The donor's backtracking reached donated slot s (frames [0, top) below it,
+// donations dst[0, nd) still live): reclaim it if no helper took it
+// (TAKE_LOCAL: search the branch here); take the helper's result if it has
+// finished (its payload readable after the acquire); else hand the rest of
+// this search to the helper (TAKE_HANDED: the caller ends without publishing
+// -- see "Hand-off").  A search whose own task was cancelled passes the
+// cancellation on and returns TAKE_CANCELLED.  Before a hand-off the donor's
+// counters and busy ticks go into its row (the helper adds to the same row).
+template <int K, typename C>
+__device__ int take_donation(const ScanArgs &A, const SLds<K, C> &S, int s, int top, const int32_t *dst, int nd,
+                             int task, int64_t *ctr, Ctr32 &c, bool &flushed, uint64_t t_start) {
     const SlotRef r = slot_ref(A, s);
+    const int ln = lane_id_here();
     uint32_t prev = 0;
-    if (lane_id_here() == 0) prev = cas_agent(&r.f->state, slot_state(A, SL_PENDING), slot_state(A, SL_RECLAIMED));
+    if (ln == 0) prev = cas_agent(&r.f->state, slot_state(A, SL_PENDING), slot_state(A, SL_RECLAIMED));
     if (uniform_u32(prev) == slot_state(A, SL_PENDING)) {
-        if (lane_id_here() == 0) add_agent(&A.split->reclaims, 1u);
+        if (ln == 0) add_agent(&A.split->reclaims, 1u);
         return TAKE_LOCAL;
     }
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        if (uniform_u32(ld_agent(&r.f->state)) == slot_state(A, SL_DONE)) break;
-        if (mine && uniform_u32(ld_agent(const_cast<uint32_t *>(&mine->cancel)))) {
-            if (lane_id_here() == 0) st_agent(&r.f->cancel, 1u);
+    if (uniform_u32(ld_agent(&r.f->state)) != slot_state(A, SL_DONE)) {
+        if (task >= 0 && uniform_u32(ld_agent(&slot_ref(A, task).f->cancel))) {
+            if (ln == 0) st_agent(&r.f->cancel, 1u);
             return TAKE_CANCELLED;
         }
-        __builtin_amdgcn_s_sleep(8);
-    }
-    const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
-    if (lane_id_here() == 0) {
-        add_agent(&ctr[SATMI_CTR_TICKS], -(int64_t)dt);
-        add_agent(&A.split->wait_ticks, (unsigned long long)dt);
+        flush_counters(ctr, c, flushed);
+        unsigned char *cont = (unsigned char *)r.f + A.split->cont_off;
+        const int fb = A.split->cont_fb;
+        put_words((uint32_t *)cont, S.fvar, top * (int)sizeof(C));
+        put_words((uint32_t *)(cont + fb), S.ftrail, top * (int)sizeof(C));
+        int32_t *cd = (int32_t *)(cont + 2 * fb);
+        for (int i = ln; i < nd; i += 64) st_agent(&cd[i], dst[i]);
+        if (ln == 0) {
+            st_agent(&r.h->cont_task, task);
+            st_agent(&r.h->cont_depth, top);
+            st_agent(&r.h->cont_nd, nd);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (ln == 0) prev = cas_agent(&r.f->state, slot_state(A, SL_RUNNING), slot_state(A, SL_HANDED));
+        if (uniform_u32(prev) == slot_state(A, SL_RUNNING)) {
+            if (ln == 0) {
+                add_agent(&ctr[SATMI_CTR_TICKS], (int64_t)(__builtin_amdgcn_s_memrealtime() - t_start));
+                add_agent(&A.split->handoffs, 1ull);
+            }
+            return TAKE_HANDED;
+        }
+        // (the helper published meanwhile: take its result)
     }
     acquire_agent();
     return uniform_i32(r.h->status) == SATMI_DPLL_STOPPED ? TAKE_SAT : TAKE_UNSAT;
@@ -1246,15 +1292,39 @@ __device__ void merge_counters(int64_t *ctr, Ctr32 &c, bool &flushed, const Slot
     }
 }
 
+// A model (ml trail codes at `src`, a slot's trail) as the first model of
+// search identity `task` of instance b: into that task's slot, or (task < 0)
+// the instance's first solution row.
+template <typename C>
+__device__ void deliver_model(const ScanArgs &A, int b, int task, const uint32_t *src, int ml) {
+    const int lh = lane_id_here();
+    if (task >= 0) {
+        const SlotRef me = slot_ref(A, task);
+        for (int i = lh; 4 * i < ml * (int)sizeof(C); i += 64) st_agent(&me.trail[i], src[i]);
+        if (lh == 0) st_agent(&me.h->model_len, ml);
+    } else if (A.sol_cap > 0) {
+        const C *mt = (const C *)src;
+        int32_t *out = A.sol_lits + (int64_t)b * A.sol_cap * A.sol_stride;
+        for (int i = lh; i < ml; i += 64) {
+            const uint32_t code = mt[i];
+            out[i] = (code & 1u) ? -(int)(code >> 1) : (int)(code >> 1);
+        }
+        if (lh == 0) A.sol_len[(int64_t)b * A.sol_cap] = ml;
+    }
+}
+
+constexpr int STATUS_HANDED = -1;   // (internal) the search was handed to a helper: nothing to publish
+
 // Search instance b from its root (task < 0: results into the instance's
 // rows), or the donated subtree of split slot `task` (results into the slot).
-// dst: this wave's donation stack.
+// dst: this wave's donation stack.  Returns whether a root search of the
+// launch finished here (its own, or a donor's handed over to this wave).
 template <int K, bool INC, typename C, bool SPLIT>
-__device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, int task, int32_t *dst) {
+__device__ bool solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, int task, int32_t *dst) {
     SplitCfg *const SPL = SPLIT ? A.split : nullptr;
     using W = typename Pack<K>::W;
     constexpr uint32_t DON = SLds<K, C>::PHASE_BIT;   // ftrail: the frame's False branch was donated
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const int ln = lane_id();
     PhaseClock ph;
     ph.start();
@@ -1263,7 +1333,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     const int mpad = padded_clauses(m);
     const int L = A.clause_lit_begin[ce] - A.clause_lit_begin[cb];
     const int n = A.inst_nvars[b];
-    const bool is_task = SPLIT && task >= 0;   // the unsplit form has no donated tasks
+    bool is_task = SPLIT && task >= 0;   // the unsplit form has no donated tasks
     int64_t *ctr = is_task ? slot_ref(A, task).h->ctr : A.counters + (int64_t)b * SATMI_NCOUNTERS;
     bool bad = m > A.lay.mcap || n > A.lay.ncap || n < 0 || L > 65535 || (INC && L > (sizeof(C) == 1 ? A.occ_cap : A.occ_lists));
     if (!bad) {
@@ -1304,7 +1374,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
             A.status[b] = SATMI_DPLL_TOO_LARGE;
             if (A.root_len) A.root_len[b] = 0;
         }
-        return;
+        return !is_task;
     }
     wave_sync();
     if constexpr (INC) build_occurrences<K>(S, const_cast<uint16_t *>(S.occ), m, n);
@@ -1367,6 +1437,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
         wave_sync();
     }
 
+    for (;;) {   // (split form) a continuation handed to this wave runs the search loop again
     while (state != ST_DONE) {
         if (state == ST_PROPAGATE) {
             const bool conflict = propagate<K, INC, C>(S, mpad, tl, nu, dec_round, ep, c.props, c.rounds, ph);
@@ -1476,7 +1547,12 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                     --nd;
                     const int s = uniform_i32(dst[nd]);
                     if (lane_id_here() == 0) S.ftrail[top] = (C)ft;
-                    const int got = take_donation(A, s, is_task ? slot_ref(A, task).f : nullptr, ctr);
+                    const int got = take_donation<K>(A, S, s, top, dst, nd, is_task ? task : -1, ctr, c, flushed,
+                                                     t_start);
+                    if (got == TAKE_HANDED) {   // the helper continues this search (see "Hand-off")
+                        status = STATUS_HANDED;
+                        break;
+                    }
                     if (got == TAKE_CANCELLED) {
                         status = SATMI_DPLL_TIMEOUT;
                         break;
@@ -1489,21 +1565,7 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
                             continue;
                         }
                         // SAT: the helper's model is the search's first model
-                        const int ml = uniform_i32(r.h->model_len);
-                        const int lh = lane_id_here();
-                        if (is_task) {
-                            const SlotRef me = slot_ref(A, task);
-                            for (int i = lh; 4 * i < ml * (int)sizeof(C); i += 64) st_agent(&me.trail[i], r.trail[i]);
-                            if (lh == 0) st_agent(&me.h->model_len, ml);
-                        } else if (A.sol_cap > 0) {
-                            const C *mt = (const C *)r.trail;
-                            int32_t *out = A.sol_lits + (int64_t)b * A.sol_cap * A.sol_stride;
-                            for (int i = lh; i < ml; i += 64) {
-                                const uint32_t code = mt[i];
-                                out[i] = (code & 1u) ? -(int)(code >> 1) : (int)(code >> 1);
-                            }
-                            if (lh == 0) A.sol_len[(int64_t)b * A.sol_cap] = ml;
-                        }
+                        deliver_model<C>(A, b, is_task ? task : -1, r.trail, uniform_i32(r.h->model_len));
                         sols = 1;
                         status = SATMI_DPLL_STOPPED;
                         break;
@@ -1557,22 +1619,81 @@ __device__ void solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     if (!is_task && A.root_lits && A.sol_stride >= 48 && ln < 24)
         ((int64_t *)(A.root_lits + (int64_t)b * A.sol_stride))[ln] = (int64_t)(ln < 8 ? ph.acc[ln] : ph.cnt[ln - 8]);
 #endif
+    if (SPLIT && status == STATUS_HANDED) return false;   // counters and ticks are in the row already
     if (SPLIT && nd > 0) cancel_donations(A, dst, nd);   // a model (or a cancellation) came first
     flush_counters(ctr, c, flushed);
     const int64_t ticks = (int64_t)(__builtin_amdgcn_s_memrealtime() - t_start);
-    if (is_task) {
+    if (!is_task) {
+        if (ln == 0) {
+            A.status[b] = status;
+            ctr[SATMI_CTR_SOLUTIONS] = sols;
+            if (SPL) add_agent(&ctr[SATMI_CTR_TICKS], ticks);
+            else ctr[SATMI_CTR_TICKS] = ticks;
+        }
+        return true;
+    }
+    if constexpr (SPLIT) {
         const SlotRef me = slot_ref(A, task);
         if (ln == 0) {
             st_agent(&me.h->status, status);
             st_agent(&ctr[SATMI_CTR_SOLUTIONS], sols);
             add_agent(&ctr[SATMI_CTR_TICKS], ticks);
         }
-        publish_state(&me.f->state, slot_state(A, SL_DONE));
-    } else if (ln == 0) {
-        A.status[b] = status;
-        ctr[SATMI_CTR_SOLUTIONS] = sols;
-        if (SPL) add_agent(&ctr[SATMI_CTR_TICKS], ticks);
-        else ctr[SATMI_CTR_TICKS] = ticks;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t prev = 0;
+        if (ln == 0) prev = cas_agent(&me.f->state, slot_state(A, SL_RUNNING), slot_state(A, SL_DONE));
+        if (uniform_u32(prev) != slot_state(A, SL_HANDED)) return false;   // published
+        // The donor handed the rest of its search to this wave: take this
+        // subtree's result as the donor would have, then go on as the donor
+        // (same instance, same trail prefix [0, tl0); see "Hand-off").
+        acquire_agent();
+        const int ctask = uniform_i32(me.h->cont_task), cdepth = uniform_i32(me.h->cont_depth);
+        const int cnd = uniform_i32(me.h->cont_nd), tl0 = uniform_i32(me.h->tl0);
+        int64_t *nctr = ctask >= 0 ? slot_ref(A, ctask).h->ctr : A.counters + (int64_t)b * SATMI_NCOUNTERS;
+        if (ln == 0) {   // this subtree's row (complete) into the donor's
+            const int k[7] = {SATMI_CTR_NODES, SATMI_CTR_DECISIONS, SATMI_CTR_UNIT_PROPS, SATMI_CTR_PURE,
+                              SATMI_CTR_CONFLICTS, SATMI_CTR_ROUNDS, SATMI_CTR_TICKS};
+            for (int i = 0; i < 7; ++i) add_agent(&nctr[k[i]], ld_agent(&ctr[k[i]]));
+        }
+        uint32_t *cont = (uint32_t *)((unsigned char *)me.f + A.split->cont_off);
+        const int fw = A.split->cont_fb / 4;
+        for (int i = lane_id_here(); 4 * i < cdepth * (int)sizeof(C); i += 64) {
+            ((uint32_t *)S.fvar)[i] = ld_agent(&cont[i]);
+            ((uint32_t *)S.ftrail)[i] = ld_agent(&cont[fw + i]);
+        }
+        for (int i = lane_id_here(); i < cnd; i += 64) st_agent(&dst[i], (int32_t)ld_agent(&cont[2 * fw + i]));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        acquire_agent();   // (the donation stack is read back with plain loads)
+        const int mine = status;
+        task = ctask;
+        is_task = ctask >= 0;
+        ctr = nctr;
+        flushed = true;
+        depth = cdepth;
+        nd = cnd;
+        sols = 0;
+        t_start = __builtin_amdgcn_s_memrealtime();
+        next_flush = next_event_after(A, 0);
+        next_event = min(next_flush, c.nodes + SPLIT_CHECK_NODES);
+        if (mine == SATMI_DPLL_STOPPED) {
+            // this subtree's model (in this slot's trail) is the donor's first model
+            deliver_model<C>(A, b, is_task ? task : -1, me.trail, uniform_i32(me.h->model_len));
+            sols = 1;
+            status = SATMI_DPLL_STOPPED;
+            state = ST_DONE;
+        } else if (mine != SATMI_DPLL_EXHAUSTED) {   // cancelled
+            status = mine;
+            state = ST_DONE;
+        } else {   // UNSAT: the donor's backtracking goes on from its trail before the donated decision
+            for (int i = tl0 + lane_id_here(); i < tl; i += 64) lv_clear(S.lv, S.trail[i] >> 1);
+            tl = tl0;
+            status = SATMI_DPLL_EXHAUSTED;
+            state = ST_BACKTRACK;
+        }
+        wave_sync();
+        continue;
+    }
+    return false;
     }
 }
 
@@ -1645,8 +1766,11 @@ __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) 
             task = w.y;
         }
         // wave-uniform (a divergent-looking b costs 64-bit VGPR address math)
-        solve_instance<K, INC, C, SPLIT>(A, S, uniform_i32(b), uniform_i32(task), dst);
-        if (SPL && ln == 0) add_agent(task < 0 ? (int32_t *)&SPL->done : &SPL->want, 1);
+        const bool root_done = solve_instance<K, INC, C, SPLIT>(A, S, uniform_i32(b), uniform_i32(task), dst);
+        if (SPL && ln == 0) {
+            if (root_done) add_agent((int32_t *)&SPL->done, 1);   // (own, or a donor's handed over)
+            if (draining) add_agent(&SPL->want, 1);                // a helper asks for its next subtree
+        }
         wave_sync();
     }
 }
@@ -1898,7 +2022,7 @@ void dpll_split_decode(const void *head, int64_t out[7]) {
     out[2] = c->claims;
     out[3] = c->reclaims;
     out[4] = c->helpers;
-    out[5] = (int64_t)c->wait_ticks;
+    out[5] = (int64_t)c->handoffs;
     out[6] = c->done;
 }
 
@@ -1963,14 +2087,17 @@ int dpll_scan_launch(const ScanLaunch &L) {
     A.snap_lds = P.fixed ? 0u : snap_lds_entries(P.lvs == 256 ? 1u : 2u, (uint32_t)lay.mcap + 1u);
     A.lay = lay;
     A.split = nullptr;
-    // split only where the launch's tail matters: fewer than SPLIT_MAX_PER_WAVE
+    // split only where the launch's tail matters: at most SPLIT_MAX_PER_WAVE
     // instances per resident wave (at 32 per wave the tail is a few percent and
-    // the two-stream pipeline hides it; the split form's register cost is not),
+    // the two-stream pipeline hides it; the split form's register cost is not;
+    // at 16 -- the N=2 shard -- the unsplit form still ran 2.5 % faster, while
+    // at 4 -- the N=8 shard -- one hard search in one rank's slice made that
+    // rank 34 % slower than the others unsplit and the split form evened them),
     // but at least one per resident wave (a launch that leaves CU slots empty
     // from the start -- configs[1]: 4,096 short searches -- loses 7 % to the
     // split form and gains nothing: the other stream's launch fills those slots)
     const int64_t waves = (int64_t)grid * waves_per_wg;
-    const bool few = L.split_always || ((int64_t)L.num_instances < (int64_t)SPLIT_MAX_PER_WAVE * waves &&
+    const bool few = L.split_always || ((int64_t)L.num_instances <= (int64_t)SPLIT_MAX_PER_WAVE * waves &&
                                         (int64_t)L.num_instances >= (int64_t)L.num_cus * P.wg_per_cu * waves_per_wg);
     if (L.split && L.split_alloc && few) {
         // slot pool: trail codes of the launch's entry width; one donation-stack
@@ -1979,7 +2106,11 @@ int dpll_scan_launch(const ScanLaunch &L) {
         const int ncap = P.fixed ? FIX_NCAP : lay.ncap;
         const int cbytes = (P.fixed || P.lvs == 256) ? 1 : 2;
         cfg.slot_bytes = slot_bytes_for(ncap, cbytes);
-        cfg.slot_cap = (int)std::min<size_t>(1u << 18, ((size_t)256 << 20) / (size_t)cfg.slot_bytes);
+        cfg.cont_off = slot_cont_off(ncap, cbytes);
+        cfg.cont_fb = slot_frames_bytes(ncap, cbytes);
+        // slots are never reused within a launch: room for the donations of a
+        // long split search (uf250 solved: ~9 * 10^4 per launch)
+        cfg.slot_cap = (int)std::min<size_t>(1u << 19, ((size_t)768 << 20) / (size_t)cfg.slot_bytes);
         cfg.dstack_cap = ncap + 1;
         cfg.max_helpers = L.num_cus * L.split_helpers_per_cu;
         cfg.warm = (uint32_t)std::max(L.split_warmup, 0);

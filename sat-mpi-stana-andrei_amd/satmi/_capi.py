@@ -52,7 +52,7 @@ SPLIT_OFF, SPLIT_AUTO, SPLIT_ALWAYS = 0, 1, 2
 
 def set_split(enable, helpers_per_cu=0):
     """Process-wide branch splitting of the clause kernels' launch tails: False/SPLIT_OFF,
-    True/SPLIT_AUTO (default: launches with at least 1 and fewer than 4 instances per resident wave) or
+    True/SPLIT_AUTO (default: launches with at least 1 and at most 8 instances per resident wave) or
     SPLIT_ALWAYS; helpers_per_cu 0 = the library default."""
     check(load().satmi_dpll_set_split(int(enable), int(helpers_per_cu)), "satmi_dpll_set_split")
 
@@ -66,7 +66,7 @@ def split_stats(stream=None):
     """Branch-splitting statistics of the last split launch on `stream` (a HIP stream handle)."""
     out = (ctypes.c_int64 * 7)()
     check(load().satmi_dpll_split_stats(stream, out), "satmi_dpll_split_stats")
-    keys = ("donations", "tickets", "claims", "reclaims", "helpers", "wait_ticks", "done")
+    keys = ("donations", "tickets", "claims", "reclaims", "helpers", "handoffs", "done")
     return dict(zip(keys, list(out)))
 
 

@@ -12,7 +12,10 @@ is a hash of the kernel's gfx950 machine code, read from the library itself:
 
 `kernel_code_sha(base)` hashes, in symbol-name order, the bytes of every
 function symbol and kernel descriptor whose name contains `base` (every
-template instance of that kernel).
+template instance of that kernel).  A descriptor's kernel_code_entry_byte_offset
+(bytes 16-23: the distance from the descriptor to the code) is zeroed first:
+it moves whenever another kernel of the same code object changes size, while
+the instructions themselves (branches are PC-relative) do not.
 """
 import hashlib
 import os
@@ -78,6 +81,8 @@ def kernel_code_sha(base, lib_path=None):
     for co in code_objects(data):
         for name, code in sorted(elf_symbols(co)):
             if base in name:
+                if name.endswith(".kd") and len(code) == 64:
+                    code = code[:16] + bytes(8) + code[24:]
                 h.update(name.encode() + b"\0" + code)
                 found = True
     return h.hexdigest()[:16] if found else None

@@ -9,6 +9,12 @@ first model:
     uuf250     uuf250-shaped random 3-SAT (n=250, m=1065), node cap 5e7: the
                UNSAT searches at n=250 that exhaust both branches of every
                decision to the end (~1 h on 5 cores)
+    5sat200    random 5-SAT n=200, m=2400 (alpha 12): configs[4]'s 5-SAT
+               batches decided to the end.  At the 5-SAT threshold (alpha
+               21.117, the node-capped bench leg) no search of 64 finished in
+               90 s on the GPU, nor at alpha 17-19 in 30 s (tools/fullsolve_probe.py,
+               profiles/r06/fullsolve_5sat_probe.txt); at alpha 12 all 64 finish
+               (77 .. 2.6e5 nodes), which the oracle can follow
     python tests/golden/make_fullsolve.py [set]      (default: uf250)
 
 The checker is the C oracle (oracle/sat_oracle.c, SOUND mode), itself pinned to
@@ -37,7 +43,8 @@ from oracle import oracle  # noqa: E402
 SETS = {"uf250": (250, 1065, 3, 250, 96, 1_200_000),
         "unsat150": (150, 639, 3, 150, 24, 2_000_000),
         "unsat200": (200, 852, 3, 200, 12, 2_000_000),
-        "uuf250": (250, 1065, 3, 2501, 16, 50_000_000)}
+        "uuf250": (250, 1065, 3, 2501, 16, 50_000_000),
+        "5sat200": (200, 2400, 5, 5200, 64, 2_000_000)}
 SET = sys.argv[1] if len(sys.argv) > 1 else "uf250"
 N, M, K, SEED, COUNT, NODE_CAP = SETS[SET]
 OUT = os.path.join(HERE, f"fullsolve_{SET}.json")

@@ -164,14 +164,17 @@ def test_configs4_batch_properties(n, m, k, cap, B):
         assert r.counter_dict(b) == {**r.counter_dict(b), **{k_: o["counters"][k_] for k_ in CTR}}
 
 
-@pytest.mark.parametrize("fixture,min_unsat", [("uf250", 0), ("unsat150", 5), ("unsat200", 5), ("uuf250", 5)])
+@pytest.mark.parametrize("fixture,min_unsat", [("uf250", 0), ("unsat150", 5), ("unsat200", 5), ("uuf250", 5),
+                                               ("5sat200", 0)])
 @pytest.mark.parametrize("split", [_capi.SPLIT_OFF, _capi.SPLIT_ALWAYS])
 def test_configs4_solved_to_completion(golden_dir, fixture, min_unsat, split):
     """configs[4]-scale searches run to the end (no node cap): uf250-shaped SAT
-    searches of 10^3-10^6 calls, UNSAT searches at n=150 / n=200, and the
+    searches of 10^3-10^6 calls, UNSAT searches at n=150 / n=200, the
     uuf250 shape itself (n=250, m=1065: 6 UNSAT searches of 2.5-8.5 M calls
     that exhaust both branches of every decision, REF.py:167-214, beside 10
-    SAT ones): status, every counter and the model equal the oracle's
+    SAT ones), and 64 random 5-SAT n=200 searches (m=2400: five 12-bit codes
+    per clause word, the 5-literal LDS layout; 77 - 2.6e5 calls each) -- all
+    decided: status, every counter and the model equal the oracle's
     (tests/golden/fullsolve_<fixture>.json, make_fullsolve.py), with and
     without branch splitting (a few searches on thousands of idle waves:
     helpers take subtrees of searches millions of calls deep).  Unsplit, a

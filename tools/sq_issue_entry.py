@@ -2,6 +2,7 @@
 (sq1 + sq2), stored in profiles/sq_issue.json for bench.py's issue_roofline().
 
     python tools/sq_issue_entry.py gpurun_out/<tag> <workload> <kernel substring> <key> <src> [keep dir] [--per-step]
+        [--isa-symbol=<mangled-name substring of the launched instance>]
 
 --per-step: a step of the workload is several launches (resolution: one pass
 kernel per saturation pass), so the counts are divided by the bench line's
@@ -29,8 +30,11 @@ CUS, SIMDS, XCDS = 256, 1024, 8
 
 
 def main():
-    argv = [a for a in sys.argv[1:] if a != "--per-step"]
+    argv = [a for a in sys.argv[1:] if a != "--per-step" and not a.startswith("--isa-symbol=")]
     per_step = "--per-step" in sys.argv
+    # the kernel instance the profiled workload launches (a mangled-name substring,
+    # e.g. dpll_scan_kernelILi3ELi512ELb1ELb0E); default: every instance of kname
+    isa_symbol = next((a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--isa-symbol=")), None)
     src, wl, kname, key, ksrc = argv[:5]
     keep = argv[5] if len(argv) > 5 else None
     vals, ndisp = {}, {}
@@ -63,9 +67,10 @@ def main():
     # rebuilding)
     sys.path.insert(0, os.path.join(ROOT, "sat-mpi-stana-andrei_amd"))
     from satmi import isa
-    isa_sha = isa.kernel_code_sha(kname.split("<")[0])
+    isa_symbol = isa_symbol or kname.split("<")[0]
+    isa_sha = isa.kernel_code_sha(isa_symbol)
     entry = {
-        "kernel": kname, "kernel_src_sha256_16": sha, "kernel_isa_sha16": isa_sha, "dispatches": nd, "profiled_kernel_ms": kms,
+        "kernel": kname, "kernel_src_sha256_16": sha, "kernel_isa_sha16": isa_sha, "isa_symbol": isa_symbol, "dispatches": nd, "profiled_kernel_ms": kms,
         "per": "step" if per_step else "launch",
         "effective_clock_hz": clock,
         "valu_insts": per("SQ_INSTS_VALU"), "salu_insts": per("SQ_INSTS_SALU"), "lds_insts": per("SQ_INSTS_LDS"),
