@@ -101,14 +101,18 @@ LEGS = [
     ("configs[3] rand-dp 8 threads", "rand-dp", ["--steps", "3", "--warmup", "1", "--threads", "8"]),
     ("configs[4] uf250", "uf250", ["--steps", "4", "--warmup", "1"]),
     ("configs[4] 5sat-n200", "5sat-n200", ["--steps", "4", "--warmup", "1"]),
-    # configs[4] solved to the end (no node limit): 512 uf250-shaped searches per
-    # step, branch splitting on with helper waves on every other CU slot
-    ("configs[4] uf250 solved", "uf250", ["--node-limit", "0", "--total", "512", "--split-always",
-                                          "--helpers-per-cu", "10", "--steps", "2", "--warmup", "0",
+    # configs[4] solved to the end (no node limit): 1,024 uf250-shaped searches per
+    # step, branch splitting on with helper waves on every free CU slot (r06
+    # sweep, profiles/r06/solved_sweep.txt: 512 per step 50.4-51.2/s at 10-24
+    # helpers per CU, 1,024 per step 54.9/s at 16)
+    ("configs[4] uf250 solved", "uf250", ["--node-limit", "0", "--total", "1024", "--split-always",
+                                          "--helpers-per-cu", "16", "--steps", "2", "--warmup", "0",
                                           "--cpu-scaled"]),
-    # 5-SAT n=200 decided to the end (alpha 12), split always
-    ("configs[4] 5sat-n200 solved", "5sat-n200-a12", ["--split-always", "--steps", "2", "--warmup", "1",
-                                                     "--cpu-scaled"]),
+    # 5-SAT n=200 decided to the end (alpha 12), split always: a step's time is
+    # its hardest search's, so the batch is large (2,048 per step 172/s, 8,192
+    # 354/s, 16,384 565/s: profiles/r06/solved_sweep.txt)
+    ("configs[4] 5sat-n200 solved", "5sat-n200-a12", ["--total", "16384", "--split-always", "--steps", "1",
+                                                     "--warmup", "0", "--cpu-scaled"]),
     ("cdcl", "cdcl", ["--steps", "3", "--warmup", "1"]),
     ("cdcl 4 threads", "cdcl", ["--steps", "3", "--warmup", "1", "--threads", "4"]),
 ]

@@ -49,8 +49,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -99,7 +102,11 @@ struct DpState {
     uint64_t first_empty;            // first pair (in pair order) with an empty resolvent
     uint64_t t0;                     // s_memrealtime at the solve's start
     int32_t cur, pending, done, result, steps, overflow, set_ovf, var, d;
-    int32_t mxA, mxB, capA, capB, capR, epoch, pad;
+    int32_t mxA, mxB, capA, capB, capR, epoch;
+    int32_t skip;    // this step slot's pipeline kernels have nothing to do (an inline step ended the slot)
+    int32_t slots;   // step slots that ran (the host sizes its next batch by them)
+    uint64_t ph[8];  // wall-clock ticks of dp_pop_split_kernel's phases (SATMI_DP_PHASES=1 prints them)
+    int64_t inl_steps;   // steps run inline
 };
 
 struct ClauseList {   // one generation of the clause list
@@ -143,6 +150,8 @@ struct DpArgs {
     int trace_cap;
     int64_t step_limit, clause_limit;
     uint64_t limit_ticks;
+    int32_t inline_steps;   // steps one slot may run inside dp_pop_split_kernel (see "Inline steps")
+    int32_t pad_;
 };
 
 __device__ __forceinline__ DView cl_view(const ClauseList &L, const int32_t *arena, int64_t c) {
@@ -261,6 +270,401 @@ __global__ void __launch_bounds__(256) dp_firstpos_kernel(DpArgs A) {
 // workgroup of 1024 threads.
 constexpr int POP_THREADS = 1024;
 constexpr int POP_LDS = 2048;   // model-set table slots kept in LDS (cap_for(V) <= this: V <= 255)
+
+// ---- Inline steps.  Most steps of a solve are small (PHP(6,5): 22 of its 30
+// steps resolve <= 5,400 pairs; the other 8 up to 3.3 * 10^5), and a small
+// step is nine kernel launches of a few microseconds each -- a dependent chain
+// whose latency, not its work, is the step's time.  So a step whose pairs fit
+// one workgroup runs to its end inside dp_pop_split_kernel, with barriers
+// between the phases instead of launch boundaries, and the kernel goes on to
+// the next step's pop while the steps stay small; the first step that does
+// not fit is split and left to the pipeline kernels queued behind (S->skip
+// tells them whether the slot left them a step).  The phases restate the
+// pipeline's exactly: resolvent keys in pair order, the first pair of each
+// distinct key as its representative (a hash table with atomicMin), the rem
+// subset test, the earlier-survivor subset test, the verdict / clause limit,
+// the kept resolvents in pair order, and the next clause list with the kept
+// resolvents' CPython set images built as dp_assemble_kernel builds them.
+constexpr int INL_PMAX = 8192;                 // pairs of an inline step
+constexpr int INL_TILE_WORDS = 4096;           // candidate-key tile of the subset tests (32 KB); the
+                                               // assembly's per-wave scratch in the same LDS
+constexpr int INL_ASM_SCRATCH = 2 * INL_TILE_WORDS / (POP_THREADS / 64);   // int32 per wave: AX, BY, R tables
+constexpr int INL_ASM_MAX = 32;                // kept resolvents assembled here (more: dp_assemble_kernel)
+struct InlLds {
+    uint32_t ntb[INL_PMAX / 32];   // non-tautological pairs
+    uint32_t flg[INL_PMAX / 32];   // representatives (by pair), dropped (by representative), hit (by survivor)
+    uint16_t ua[INL_PMAX];         // representatives' pair indices, later the kept ones (pair order)
+    uint16_t ub[INL_PMAX];         // survivors' pair indices (pair order)
+    uint64_t tile[INL_TILE_WORDS];
+    uint32_t fe;                   // first pair with an empty resolvent
+    int64_t arena_top;
+};
+
+// thread 0's phase clock: ticks since the last mark into S->ph[k]
+__device__ __forceinline__ void ph_mark(DpState *S, uint64_t &t, int k) {
+    if (threadIdx.x == 0) {
+        const uint64_t x = __builtin_amdgcn_s_memrealtime();
+        S->ph[k] += x - t;
+        t = x;
+    }
+}
+
+// phase boundary inside the workgroup: its waves share the CU's L1, so a
+// workgroup-scope release / acquire (waits, no cache maintenance) suffices
+__device__ __forceinline__ void wg_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// flag(x) for x in [0, n) into bitmap words: each wave's 64 consecutive x are
+// one ballot, two words written by its lane 0
+template <class F>
+__device__ __forceinline__ void inl_bits(uint32_t *words, int n, F &&flag) {
+    const int tid = threadIdx.x, lane = lane_id(), wb = 64 * (tid >> 6);
+    for (int x0 = 0; x0 < n; x0 += POP_THREADS) {
+        const int x = x0 + tid;
+        const bool b = x < n && flag(x);
+        const uint64_t m = __ballot(b);
+        if (lane == 0 && x0 + wb < n) {
+            words[(x0 + wb) >> 5] = (uint32_t)m;
+            words[((x0 + wb) >> 5) + 1] = (uint32_t)(m >> 32);
+        }
+    }
+}
+
+// the set (want = 1) or clear (want = 0) bits of words [0, n) in order:
+// out[k] = val(x) of the k-th such x; returns their count (every thread)
+template <class F>
+__device__ __forceinline__ int inl_compact(const uint32_t *words, int n, int want, uint16_t *out, int *wsum, F &&val) {
+    const int tid = threadIdx.x, nw = (n + 31) >> 5;
+    uint32_t m = 0;
+    if (tid < nw) {
+        m = want ? words[tid] : ~words[tid];
+        const int rest = n - 32 * tid;
+        if (rest < 32) m &= (1u << rest) - 1u;
+    }
+    int total;
+    int off = block_excl_scan(__popc(m), wsum, total);
+    while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1u;
+        out[off++] = (uint16_t)val(32 * tid + b);
+    }
+    wg_sync();
+    return total;
+}
+
+__device__ __forceinline__ bool key_subset(const uint64_t *y, const uint64_t *x, int K) {
+    uint64_t o = 0;
+    for (int w = 0; w < K; ++w) o |= y[w] & ~x[w];
+    return o == 0ull;
+}
+
+// L.flg bit x (x < nx) = some candidate y (y < ny; earlier = only y < x) is
+// a subset of x's key.  The candidates' keys go through LDS in tiles and
+// every lane reads the same tile
+// entry at a time (a broadcast), x's key in registers (K <= INL_KMAX words);
+// a tile loop ends once no x of the workgroup is still open.
+constexpr int INL_KMAX = 8;
+template <int KT, class FX, class FY>   // KT: key words known at compile time (0: Kr, up to INL_KMAX)
+__device__ void inl_tests(InlLds &L, int nx, int ny, int Kr, bool earlier, FX &&xkey, FY &&ykey, uint32_t &tests) {
+    constexpr int KR = KT ? KT : INL_KMAX;   // key words held in registers
+    const int K = KT ? KT : Kr;
+    const int tid = threadIdx.x;
+    uint64_t *tile = L.tile;
+    const int tcap = INL_TILE_WORDS / K;   // keys per tile
+    for (int x0 = 0; x0 < nx; x0 += POP_THREADS) {
+        const int x = x0 + tid;
+        bool open = x < nx;
+        bool hit = false;
+        uint64_t xk[KR];
+#pragma unroll
+        for (int w = 0; w < KR; ++w) xk[w] = (open && w < K) ? xkey(x)[w] : ~0ull;
+        // candidates that can matter to this chunk: all, or those before its last x
+        const int yend = earlier ? min(ny, x0 + POP_THREADS) : ny;
+        for (int y0 = 0; y0 < yend; y0 += tcap) {
+            const int cnt = min(tcap, yend - y0);
+            __syncthreads();   // the previous tile is no longer read
+            for (int e = tid; e < cnt * K; e += POP_THREADS) tile[e] = ykey(y0 + e / K)[e % K];
+            wg_sync();
+            if (open) {
+                const int lim = earlier ? min(cnt, x - y0) : cnt;
+                int j = 0;
+                for (; j < lim; ++j) {
+                    uint64_t o = 0;
+#pragma unroll
+                    for (int w = 0; w < KR; ++w)
+                        if (KT || w < K) o |= tile[j * K + w] & ~xk[w];
+                    if (o == 0ull) {
+                        hit = true;
+                        ++j;
+                        break;
+                    }
+                }
+                tests += (uint32_t)max(j, 0);
+                if (hit || (earlier && y0 + cnt >= x)) open = false;
+            }
+            if (!__syncthreads_or(open)) break;
+        }
+        const uint64_t m = __ballot(hit);
+        const int wb = 64 * (tid >> 6);
+        if (lane_id() == 0 && x0 + wb < nx) {
+            L.flg[(x0 + wb) >> 5] = (uint32_t)m;
+            L.flg[((x0 + wb) >> 5) + 1] = (uint32_t)(m >> 32);
+        }
+    }
+    wg_sync();
+}
+
+// inl_tests with the key width as a constant for one-word-per-sign keys (<= 64
+// variables: every configs[3] formula), else up to INL_KMAX words at run time
+#define INL_TESTS_K(K, L_, NX, NY, EARLIER, FX, FY, T)                  \
+    do {                                                                \
+        if ((K) == 2) inl_tests<2>(L_, NX, NY, K, EARLIER, FX, FY, T);  \
+        else inl_tests<0>(L_, NX, NY, K, EARLIER, FX, FY, T);           \
+    } while (0)
+constexpr int64_t INL_TESTS_MAX = 1 << 18;   // subset tests of a phase run inline (~2 per ns on one CU)
+
+__device__ __forceinline__ uint64_t inl_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// One elimination step of the current split (g[cur], plist / nlist / rlist /
+// rkeys), phases of dp_pairs .. dp_assemble in one workgroup.  Returns 1 when
+// the solve ends here (an empty resolvent or the clause limit), 2 when the
+// assembly of the next list is left to dp_assemble_kernel (S->skip = 2), else
+// 0 with lfp (the first-position table in LDS, V <= FP_LDS) holding the next
+// list's.
+__device__ int dp_inline_step(const DpArgs &A, DpState *S, InlLds &L, int *wsum, unsigned long long *lfp, int cur,
+                               int64_t np, int64_t nn, int64_t nr, int32_t var, int d, int capA, int capB, int capR,
+                               uint64_t &tclk) {
+    const int tid = threadIdx.x;
+    const int K = A.K, W = A.W;
+    const ClauseList CL = A.g[cur], O = A.g[cur ^ 1];
+    const int P = (int)(np * nn);
+    const uint64_t vb = 1ull << (d & 63);
+    const int vw = d >> 6;
+    if (tid == 0) L.fe = DP_EMPTY >> 32;
+    wg_sync();
+    // pairs (dp_pairs_kernel): resolvent keys, tautology / empty flags
+    int ntc = 0;
+    inl_bits(L.ntb, P, [&](int p) {
+        const int i = p / (int)nn, j = p - i * (int)nn;
+        const uint64_t *a = CL.bits + A.plist[i] * K, *b = CL.bits + A.nlist[j] * K;
+        uint64_t *r = A.rbits + (uint64_t)p * K;
+        bool taut = false, empty = true;
+        for (int w = 0; w < W; ++w) {
+            const uint64_t keep = w == vw ? ~vb : ~0ull;
+            const uint64_t rp = (a[w] & keep) | b[w], rn = a[W + w] | (b[W + w] & keep);
+            r[w] = rp;
+            r[W + w] = rn;
+            taut |= (rp & rn) != 0ull;
+            empty &= (rp | rn) == 0ull;
+        }
+        if (empty) atomicMin(&L.fe, (uint32_t)p);
+        ntc += (!taut && !empty) ? 1 : 0;
+        return !taut && !empty;
+    });
+    const int nontaut = block_sum(ntc, wsum);
+    wg_sync();
+    ph_mark(S, tclk, 1);
+    const uint32_t fe = L.fe;
+    const auto nt = [&](int p) { return ((L.ntb[p >> 5] >> (p & 31)) & 1u) != 0u; };
+    uint32_t tests = 0;   // (statistics; wraps past 2^32 per thread)
+    int nuniq = 0, ns = 0, nkept = 0;
+    if (fe == (uint32_t)(DP_EMPTY >> 32)) {
+        // distinct resolvents (dp_hash_kernel): the smallest pair index per key
+        for (int p = tid; p < P; p += POP_THREADS) {
+            if (!nt(p)) continue;
+            const uint64_t *x = A.rbits + (uint64_t)p * K;
+            uint64_t h = 0x9E3779B97F4A7C15ull;
+            for (int w = 0; w < K; ++w) h = inl_mix64(h ^ x[w]) + (uint64_t)w;
+            uint64_t sl = h & A.tmask;
+            for (;;) {
+                uint64_t c = __hip_atomic_load(A.table + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (c == DP_EMPTY) {
+                    c = atomicCAS((unsigned long long *)(A.table + sl), (unsigned long long)DP_EMPTY,
+                                  (unsigned long long)p);
+                    if (c == DP_EMPTY) break;
+                }
+                if (key_subset(A.rbits + c * K, x, K) && key_subset(x, A.rbits + c * K, K)) {
+                    if ((uint64_t)p < c) atomicMin((unsigned long long *)(A.table + sl), (unsigned long long)p);
+                    break;
+                }
+                sl = (sl + 1) & A.tmask;
+            }
+            A.uslot[p] = (uint32_t)sl;
+        }
+        wg_sync();
+        inl_bits(L.flg, P, [&](int p) {
+            return nt(p) && __hip_atomic_load(A.table + A.uslot[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                (uint64_t)p;
+        });
+        wg_sync();
+        nuniq = inl_compact(L.flg, P, 1, L.ua, wsum, [](int p) { return p; });
+        for (int k = tid; k < nuniq; k += POP_THREADS)   // the table clean for the next step
+            __hip_atomic_store(A.table + A.uslot[L.ua[k]], DP_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ph_mark(S, tclk, 2);
+        // rem test (dp_remtest_kernel): dropped when a remaining clause is a
+        // subset.  One CU runs ~2 tests per ns: a step with many tests leaves
+        // here (nothing it did matters to the pipeline, which redoes the step)
+        if ((int64_t)nuniq * nr > INL_TESTS_MAX) return 3;
+        const auto rx = [&](int u) { return A.rbits + (uint64_t)L.ua[u] * K; };
+        const auto ry = [&](int j) { return A.rkeys + (uint64_t)j * K; };
+        INL_TESTS_K(K, L, nuniq, (int)nr, false, rx, ry, tests);
+        ns = inl_compact(L.flg, nuniq, 0, L.ub, wsum, [&](int u) { return (int)L.ua[u]; });
+        if ((int64_t)ns * ns / 2 > INL_TESTS_MAX) return 3;
+        ph_mark(S, tclk, 3);
+        // survivor test (dp_survtest_kernel): hit by an earlier survivor (pair order)
+        const auto sx = [&](int k) { return A.rbits + (uint64_t)L.ub[k] * K; };
+        INL_TESTS_K(K, L, ns, ns, true, sx, sx, tests);
+        ph_mark(S, tclk, 4);
+    }
+    // the verdict (dp_kept_kernel): the first empty resolvent or the clause
+    // limit (the kth non-tautological non-empty pair), whichever comes first
+    int64_t limit_pair = -1;
+    const int64_t kth = max<int64_t>(A.clause_limit - nr, 0);
+    if (A.clause_limit > 0 && nontaut > kth) {
+        int c = tid < ((P + 31) >> 5) ? __popc(L.ntb[tid] & (P - 32 * tid < 32 ? (1u << (P - 32 * tid)) - 1u : ~0u))
+                                        : 0;
+        int tot;
+        const int ex = block_excl_scan(c, wsum, tot);
+        if (tid == 0) L.arena_top = -1;
+        wg_sync();
+        if (kth >= ex && kth < ex + c) {
+            uint32_t m = L.ntb[tid];
+            for (int64_t need = kth - ex; need > 0; --need) m &= m - 1u;
+            L.arena_top = 32 * tid + __builtin_ctz(m);   // (borrowed: the limit pair)
+        }
+        wg_sync();
+        limit_pair = L.arena_top;
+        wg_sync();
+    }
+    const uint32_t ttests = (uint32_t)block_sum((int)tests, wsum);
+    if (fe != (uint32_t)(DP_EMPTY >> 32) || limit_pair >= 0) {
+        if (tid == 0) {
+            S->nontaut = nontaut;
+            S->tests += ttests;
+            S->first_empty = fe == (uint32_t)(DP_EMPTY >> 32) ? DP_EMPTY : (uint64_t)fe;
+            S->result = (fe != (uint32_t)(DP_EMPTY >> 32) && (limit_pair < 0 || (int64_t)fe < limit_pair)) ? 0 : -1;
+            S->done = 1;
+        }
+        return 1;
+    }
+    nkept = inl_compact(L.flg, ns, 0, L.ua, wsum, [&](int k) { return (int)L.ub[k]; });
+    const int64_t ncl2 = nr + nkept;
+    ph_mark(S, tclk, 5);
+    if (tid == 0) S->inl_steps += 1;
+    // many kept resolvents: their images (a serial chain of CPython set
+    // operations each) are built by the pipeline's assemble kernel across the
+    // GPU, one wave each; a few are built here, one wave each in LDS
+    const bool here = nkept <= INL_ASM_MAX && 2 * (capA + capB + capR) <= INL_ASM_SCRATCH;
+    if (tid == 0) {
+        const int64_t base = S->arena_top;
+        L.arena_top = base;
+        S->nontaut = nontaut;
+        S->nuniq = nuniq;
+        S->nsurv = ns;
+        S->nkept = nkept;
+        S->tests += ttests;
+        S->ncl2 = ncl2;
+        S->arena_base = base;
+        S->arena_top = base + (int64_t)nkept * 2 * capR;
+        S->new_total += nontaut;
+        S->pending = 1;
+        if (!here) S->skip = 2;   // the slot's kernels: only dp_assemble_kernel runs
+    }
+    if (!here) {
+        for (int k = tid; k < nkept; k += POP_THREADS) A.klist[k] = L.ua[k];
+        return 2;
+    }
+    for (int x = tid; x < A.V; x += POP_THREADS) lfp[x] = ~0ull;
+    wg_sync();
+    // the next clause list (dp_assemble_kernel): rem clauses, then the kept
+    // resolvents' images built by lane 0 of a wave in its LDS scratch
+    const int lane = lane_id(), wid = tid >> 6;
+    const int64_t base = L.arena_top;
+    for (int64_t t = tid; t < nr; t += POP_THREADS) {   // rem clauses: one per thread
+        const int64_t c = A.rlist[t];
+        const int64_t off = CL.off[c];
+        const int32_t mask = CL.mask[c];
+        O.off[t] = off;
+        O.mask[t] = mask;
+        O.fill[t] = CL.fill[c];
+        O.used[t] = CL.used[c];
+        for (int w = 0; w < K; ++w) O.bits[t * K + w] = CL.bits[c * K + w];
+        const int32_t *img = A.arena + off;
+        for (int32_t x = 0; x <= mask; ++x) {   // first positions (REF.py:128's comprehension order)
+            const int32_t key = img[x];
+            if (key == PY_EMPTY || key == PY_DUMMY) continue;
+            atomicMin(&lfp[A.v2d[key < 0 ? -key : key]], ((unsigned long long)t << 32) | (unsigned long long)x);
+        }
+    }
+    for (int64_t t = nr + wid; t < ncl2; t += POP_THREADS / 64) {   // kept resolvents: one per wave
+        const int32_t *img;
+        int64_t mask;
+        {
+            const int64_t k = t - nr;
+            const uint32_t p = L.ua[k];
+            int32_t *xa = (int32_t *)L.tile + wid * INL_ASM_SCRATCH;
+            int32_t *xb = xa + 2 * capA;
+            int32_t *ra = xb + 2 * capB;
+            int32_t *dst = A.arena + base + k * 2 * capR;
+            int64_t rm = 0, rf = 0, ru = 0, roff = 0;
+            if (lane == 0) {
+                const uint32_t i = p / (uint32_t)nn, j = p - i * (uint32_t)nn;
+                DSet ax, by, r;
+                dset_init(ax, xa, xa + capA, capA);
+                py_difference1(ax, cl_view(CL, A.arena, A.plist[i]), var);    // pc - {var}
+                dset_init(by, xb, xb + capB, capB);
+                py_difference1(by, cl_view(CL, A.arena, A.nlist[j]), -var);   // nc - {-var}
+                dset_init(r, ra, ra + capR, capR);
+                py_merge(r, dset_view(ax));   // set_copy(AX)
+                py_merge(r, dset_view(by));   // |= BY
+                if (ax.overflow || by.overflow || r.overflow) S->set_ovf = 1;
+                rm = r.mask;
+                rf = r.fill;
+                ru = r.used;
+                roff = r.t - ra;
+            }
+            wave_sync();
+            rm = __shfl(rm, 0);
+            rf = __shfl(rf, 0);
+            ru = __shfl(ru, 0);
+            roff = __shfl(roff, 0);
+            const int32_t *src = ra + roff;
+            for (int64_t x = lane; x <= rm; x += 64) dst[x] = src[x];
+            if (lane == 0) {
+                O.off[t] = dst - A.arena;
+                O.mask[t] = (int32_t)rm;
+                O.fill[t] = (int32_t)rf;
+                O.used[t] = (int32_t)ru;
+            }
+            if (lane < K) O.bits[t * K + lane] = A.rbits[(uint64_t)p * K + lane];
+            img = src;
+            mask = rm;
+        }
+        for (int64_t x = lane; x <= mask; x += 64) {   // first positions (REF.py:128's comprehension order)
+            const int32_t key = img[x];
+            if (key == PY_EMPTY || key == PY_DUMMY) continue;
+            atomicMin(&lfp[A.v2d[key < 0 ? -key : key]], ((unsigned long long)t << 32) | (unsigned long long)x);
+        }
+        wave_sync();   // the wave's scratch is rewritten by its next clause
+    }
+    wg_sync();
+    for (int x = tid; x < A.V; x += POP_THREADS)   // (the pipeline's next pop reads them from memory)
+        if (lfp[x] != ~0ull) atomicMin(&A.firstpos[x], lfp[x]);
+    ph_mark(S, tclk, 6);
+    return 0;
+}
+
+// INL: the form with inline steps (opt-in, SATMI_DP_INLINE=1: measured slower
+// than the pipeline); the default form has none of that code
+// (its register budget is the pop / split's alone)
+template <bool INL>
 __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
     __shared__ unsigned long long fp_sh[FP_LDS];
     __shared__ int32_t ord_sh[FP_LDS];
@@ -268,22 +672,30 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
     __shared__ int wsum[16];
     __shared__ int64_t sh_ncl;
     __shared__ int sh_cur, sh_quit, sh_var;
+    __shared__ std::conditional_t<INL, InlLds, char> inl;
     DpState *S = A.st;
     if (S->done) return;
     const int tid = threadIdx.x;
+    const int V = A.V;
+    const bool lds_fp = V <= FP_LDS;
+    uint64_t tclk = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0;; ++it) {
     if (tid == 0) {
         if (S->pending) {   // the previous step's generation becomes the clause list
             S->cur ^= 1;
             S->ncl = S->ncl2;
             S->pending = 0;
         }
+        if (it == 0) {
+            S->skip = 0;
+            S->slots += 1;
+        }
         sh_cur = S->cur;
         sh_ncl = S->ncl;
         sh_quit = 0;
     }
-    const int V = A.V;
-    const bool lds_fp = V <= FP_LDS;
-    if (lds_fp)
+    // (after an inline step its first-position table is already in fp_sh)
+    if (lds_fp && it == 0)
         for (int d = tid; d < V; d += POP_THREADS) fp_sh[d] = A.firstpos[d];
     __syncthreads();
     // the variables that occur: their count and range
@@ -446,6 +858,30 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
     }
     for (int e = tid; e < V; e += POP_THREADS) A.firstpos[e] = ~0ull;   // for the next step's assembly
     if (tid < 3 * DP_STRIPES) A.stripes[tid] = 0ull;
+    if constexpr (!INL) {
+        (void)inl;
+        (void)tclk;
+        return;
+    } else {
+    // run this step here (Inline steps) if it fits the workgroup; else the
+    // pipeline kernels queued behind this one run it
+    const int capA = (int)cap_for(mxA), capB = (int)cap_for(mxB), capR = (int)cap_for((int64_t)mxA + mxB);
+    if (tid == 0) {
+        const bool fit = it < A.inline_steps && npairs <= INL_PMAX && lds_fp && K <= INL_KMAX &&
+                         nr + npairs <= A.ncl_cap && S->arena_top + npairs * 2 * capR <= A.arena_cap;
+        sh_quit = fit ? 0 : 1;
+    }
+    wg_sync();
+    ph_mark(S, tclk, 0);
+    if (sh_quit) return;
+    if (dp_inline_step(A, S, inl, wsum, fp_sh, sh_cur, np, nn, nr, var, d, capA, capB, capR, tclk)) return;   // 1, 2
+    wg_sync();
+    if (it + 1 >= A.inline_steps) {   // (recording: one step per slot) the slot's pipeline kernels skip
+        if (tid == 0) S->skip = 1;
+        return;
+    }
+    }
+    }
 }
 
 // pair p = i*nn + j: resolvent key, tautology (REF.py:115) and empty (REF.py:117)
@@ -454,6 +890,7 @@ __global__ void __launch_bounds__(256) dp_pairs_kernel(DpArgs A) {
     __shared__ int wsum[4];
     DpState *S = A.st;
     if (S->done) return;
+    if (S->skip) return;
     const uint32_t npairs = (uint32_t)S->npairs, nn = (uint32_t)S->nn;
     const int d = S->d, W = A.W, K = A.K;
     const ClauseList L = A.g[S->cur];
@@ -500,7 +937,7 @@ __device__ __forceinline__ uint64_t dp_mix64(uint64_t z) {
 // claim goes to uslot.
 __global__ void __launch_bounds__(256) dp_hash_kernel(DpArgs A) {
     DpState *S = A.st;
-    if (S->done || S->first_empty != DP_EMPTY) return;   // the step ends in an empty clause
+    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;   // the step ends in an empty clause
     const uint32_t npairs = (uint32_t)S->npairs;
     const int K = A.K, lane = lane_id();
     for (uint32_t p0 = blockIdx.x * 256u + (threadIdx.x & ~63u); p0 < npairs; p0 += gridDim.x * 256u) {
@@ -633,7 +1070,7 @@ template <int KT>
 __global__ void __launch_bounds__(TEST_TILE) dp_remtest_kernel(DpArgs A) {
     __shared__ int wsum[4];
     DpState *S = A.st;
-    if (S->done || S->first_empty != DP_EMPTY) return;
+    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;
     int tests = 0;
     dp_test_items<KT, false>(A, S->nuniq, S->nr, A.ukeys, A.rkeys, nullptr, A.dropped, S->epoch, tests);
     const int tot = block_sum(tests, wsum);
@@ -646,7 +1083,7 @@ __global__ void __launch_bounds__(TEST_TILE) dp_remtest_kernel(DpArgs A) {
 __global__ void __launch_bounds__(256) dp_gather_kernel(DpArgs A) {
     __shared__ int64_t pre[DP_STRIPES + 1];
     DpState *S = A.st;
-    if (S->done || S->first_empty != DP_EMPTY) return;
+    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;
     if (threadIdx.x == 0) {
         int64_t acc = 0;
         for (int t = 0; t < DP_STRIPES; ++t) {
@@ -671,7 +1108,7 @@ __global__ void __launch_bounds__(256) dp_gather_kernel(DpArgs A) {
 // every used table slot cleared for the next step
 __global__ void __launch_bounds__(256) dp_survlist_kernel(DpArgs A) {
     DpState *S = A.st;
-    if (S->done || S->first_empty != DP_EMPTY) return;
+    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;
     const int64_t nuniq = S->nuniq;
     const int32_t epoch = S->epoch;
     const int lane = lane_id(), K = A.K, tid = threadIdx.x;
@@ -711,7 +1148,7 @@ template <int KT>
 __global__ void __launch_bounds__(TEST_TILE) dp_survtest_kernel(DpArgs A) {
     __shared__ int wsum[4];
     DpState *S = A.st;
-    if (S->done || S->first_empty != DP_EMPTY) return;
+    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;
     int tests = 0;
     dp_test_items<KT, true>(A, S->nsurv, S->nsurv, A.skeys, A.skeys, A.surv, A.hit, S->epoch, tests);
     const int tot = block_sum(tests, wsum);
@@ -725,7 +1162,7 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
     __shared__ int wsum[16];
     __shared__ int64_t sh_lim;
     DpState *S = A.st;
-    if (S->done) return;
+    if (S->done || S->skip) return;
     const int tid = threadIdx.x;
     const uint64_t fe = S->first_empty;
     __shared__ int64_t sh_nt;
@@ -851,6 +1288,7 @@ __global__ void __launch_bounds__(64 * ASM_WAVES) dp_assemble_kernel(DpArgs A) {
     __shared__ int32_t scratch_sh[ASM_WAVES][ASM_SCRATCH];
     DpState *S = A.st;
     if (S->done) return;
+    if (S->skip == 1) return;   // (2: an inline step left this kernel its assembly)
     unsigned long long *lfp = A.V <= FP_LDS ? lfp_sh : nullptr;
     firstpos_begin(A, lfp);
     const int cur = S->cur;
@@ -1027,6 +1465,8 @@ struct DpWork {
     uint64_t tslots = 0;
     int K = 0;
     int32_t epoch = 0;
+    DpArgs hint_args;             // the last completed call's arguments and step slots used
+    int hint_slots = 0;
     std::vector<hipEvent_t> ev;   // filter timing: one pair per step, read once per call
     hipStream_t stream = nullptr;
     DpState *pin = nullptr;       // pinned host copy of the state
@@ -1250,6 +1690,9 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
 
     double hz = 1e8;
     (void)satmi_wallclock_hz(&hz);
+    const bool record = h_rec_lits && h_rec_clause_off && h_rec_step_off;
+    const char *inl_env = std::getenv("SATMI_DP_INLINE");
+    const bool inline_on = inl_env && inl_env[0] == '1';
     const auto args = [&]() {
         DpArgs a;
         std::memset(&a, 0, sizeof(a));   // padding too: a batch's graph is keyed by these bytes
@@ -1294,6 +1737,9 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         a.step_limit = step_limit;
         a.clause_limit = clause_limit;
         a.limit_ticks = time_limit_s > 0 ? (uint64_t)std::max(1.0, time_limit_s * hz) : 0;
+        // inline steps (opt-in); recording reads the clause list after every
+        // step: one step per slot
+        a.inline_steps = !inline_on ? 0 : record ? 1 : (1 << 30);
         return a;
     };
     DpArgs A = args();
@@ -1317,7 +1763,8 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
     const auto enqueue_step = [&](const DpArgs &a) -> int {
         const int gp = (int)std::min<int64_t>(DP_GRID_PAIRS, (a.pair_cap + 255) / 256);
         const int gc = (int)std::min<int64_t>(DP_GRID_ASM, (a.ncl_cap + ASM_WAVES - 1) / ASM_WAVES);
-        hipLaunchKernelGGL(dp_pop_split_kernel, dim3(1), dim3(POP_THREADS), 0, s, a);
+        if (a.inline_steps > 0) hipLaunchKernelGGL(dp_pop_split_kernel<true>, dim3(1), dim3(POP_THREADS), 0, s, a);
+        else hipLaunchKernelGGL(dp_pop_split_kernel<false>, dim3(1), dim3(POP_THREADS), 0, s, a);
         hipLaunchKernelGGL(dp_pairs_kernel, dim3(gp), dim3(256), 0, s, a);
         hipLaunchKernelGGL(dp_hash_kernel, dim3(gp), dim3(256), 0, s, a);
         hipLaunchKernelGGL(dp_gather_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(DP_GRID_GATHER, a.pair_cap / (DP_STRIPES * 256))), DP_STRIPES),
@@ -1343,15 +1790,20 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         SATMI_HIP(hipGetLastError());
         return SATMI_OK;
     };
-    const bool record = h_rec_lits && h_rec_clause_off && h_rec_step_off;
     int64_t rec_clauses = 0, rec_lits = 0;
     int recorded_steps = 0;
     std::vector<int64_t> h_off;
     std::vector<int32_t> h_mask, h_arena;
     int enqueued = 0;   // steps enqueued since the last resume
+    bool first_batch = true;
     for (;;) {
-        // at most V steps eliminate a variable, then one pop finds the set empty
-        const int batch = record ? 1 : std::min(64, V + 1);
+        // at most V steps eliminate a variable, then one pop finds the set empty;
+        // a slot may run many steps inline, so a call with the arguments of the
+        // last one starts with as many slots as that one used (the next batch,
+        // if any, with the full count)
+        const bool hinted = first_batch && Wk.hint_slots > 0 && std::memcmp(&Wk.hint_args, &A, sizeof(DpArgs)) == 0;
+        const int batch = record ? 1 : hinted ? std::min(Wk.hint_slots, V + 1) : std::min(64, V + 1);
+        first_batch = false;
         hipEvent_t *ev = next_events();
         if (!ev) {
             set_error("satmi_dp_host: hipEventCreate failed");
@@ -1452,6 +1904,17 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         }
     }
     Wk.epoch = st.epoch + 1;
+    if (std::getenv("SATMI_DP_PHASES")) {   // diagnostics: dp_pop_split_kernel's phase clocks (ticks of hz)
+        std::fprintf(stderr, "dp phases us: pop+split %.1f pairs %.1f dedup %.1f remtest %.1f survtest %.1f "
+                             "kept %.1f assemble %.1f | slots %d inline steps %lld of %d\n",
+                     st.ph[0] * 1e6 / hz, st.ph[1] * 1e6 / hz, st.ph[2] * 1e6 / hz, st.ph[3] * 1e6 / hz,
+                     st.ph[4] * 1e6 / hz, st.ph[5] * 1e6 / hz, st.ph[6] * 1e6 / hz, st.slots,
+                     (long long)st.inl_steps, st.steps);
+    }
+    if (!record) {   // the slots this call used: the next call's first batch
+        Wk.hint_args = A;
+        Wk.hint_slots = std::max(1, st.slots);
+    }
     const int steps = st.steps;
     if (h_trace_vars && steps > 0) {
         std::vector<int32_t> tr((size_t)steps);

@@ -196,7 +196,13 @@ __device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return
 // uf250 fits 15 searches per CU instead of 13 (+10 %).  (5-SAT n=200 gains no
 // residency from it and pays the packing's shifts: one word per code there.)
 template <int K, typename C>
-constexpr bool cnt_packed() { return sizeof(C) == 2 && K == 3; }
+constexpr bool cnt_packed() {
+#ifdef SATMI_CNT_PACK_ALL   // A/B variant: byte codes (the bench kernel) packed too
+    return K == 3;
+#else
+    return sizeof(C) == 2 && K == 3;
+#endif
+}
 template <int K, typename C>
 __device__ __forceinline__ void cnt_inc(const SLds<K, C> &S, uint32_t code, uint32_t inc) {
     if constexpr (!cnt_packed<K, C>()) atomicAdd(&S.cnt[code], inc);
@@ -1240,7 +1246,7 @@ enum { TAKE_LOCAL = 0, TAKE_UNSAT = 1, TAKE_SAT = 2, TAKE_CANCELLED = 3, TAKE_HA
 // counters and busy ticks go into its row (the helper adds to the same row).
 template <int K, typename C>
 __device__ int take_donation(const ScanArgs &A, const SLds<K, C> &S, int s, int top, const int32_t *dst, int nd,
-                             int task, int64_t *ctr, Ctr32 &c, bool &flushed, uint64_t t_start) {
+                             int task, int64_t *ctr, Ctr32 &c, bool &flushed, uint64_t &t_start) {
     const SlotRef r = slot_ref(A, s);
     const int ln = lane_id_here();
     uint32_t prev = 0;
@@ -1255,6 +1261,11 @@ __device__ int take_donation(const ScanArgs &A, const SLds<K, C> &S, int s, int 
             return TAKE_CANCELLED;
         }
         flush_counters(ctr, c, flushed);
+        // this wave's busy time so far into the row before the hand-off can be
+        // adopted (after it, the helper may publish the row at any moment)
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (ln == 0) add_agent(&ctr[SATMI_CTR_TICKS], (int64_t)(now - t_start));
+        t_start = now;   // (if the helper published first, the search goes on here from now)
         unsigned char *cont = (unsigned char *)r.f + A.split->cont_off;
         const int fb = A.split->cont_fb;
         put_words((uint32_t *)cont, S.fvar, top * (int)sizeof(C));
@@ -1269,10 +1280,7 @@ __device__ int take_donation(const ScanArgs &A, const SLds<K, C> &S, int s, int 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (ln == 0) prev = cas_agent(&r.f->state, slot_state(A, SL_RUNNING), slot_state(A, SL_HANDED));
         if (uniform_u32(prev) == slot_state(A, SL_RUNNING)) {
-            if (ln == 0) {
-                add_agent(&ctr[SATMI_CTR_TICKS], (int64_t)(__builtin_amdgcn_s_memrealtime() - t_start));
-                add_agent(&A.split->handoffs, 1ull);
-            }
+            if (ln == 0) add_agent(&A.split->handoffs, 1ull);
             return TAKE_HANDED;
         }
         // (the helper published meanwhile: take its result)
@@ -2109,8 +2117,11 @@ int dpll_scan_launch(const ScanLaunch &L) {
         cfg.cont_off = slot_cont_off(ncap, cbytes);
         cfg.cont_fb = slot_frames_bytes(ncap, cbytes);
         // slots are never reused within a launch: room for the donations of a
-        // long split search (uf250 solved: ~9 * 10^4 per launch)
-        cfg.slot_cap = (int)std::min<size_t>(1u << 19, ((size_t)768 << 20) / (size_t)cfg.slot_bytes);
+        // long split search (uf250 solved, 512 searches, 10 helpers per CU:
+        // 2.6 * 10^5 per launch; a pool of 768 MB -- 2.9 * 10^5 uf250 slots --
+        // ran dry at 16 helpers per CU and the helpers idled: 50.7 -> 9.4
+        // instances/s).  2 GiB per stream of the 288 GB.
+        cfg.slot_cap = (int)std::min<size_t>(1u << 21, ((size_t)2048 << 20) / (size_t)cfg.slot_bytes);
         cfg.dstack_cap = ncap + 1;
         cfg.max_helpers = L.num_cus * L.split_helpers_per_cu;
         cfg.warm = (uint32_t)std::max(L.split_warmup, 0);

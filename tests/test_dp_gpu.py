@@ -164,3 +164,49 @@ def test_launch_chain_floor():
     assert st["device_ms"] * 1e3 / st["launches"] >= floor
     with pytest.raises(_capi.SatmiError):
         _capi.launch_chain_floor(0)
+
+
+@pytest.fixture
+def dp_inline(monkeypatch):
+    """The opt-in inline-step form of the pop kernel (SATMI_DP_INLINE=1: small
+    steps run to their end inside one workgroup; read per call)."""
+    monkeypatch.setenv("SATMI_DP_INLINE", "1")
+    yield
+
+
+def test_inline_steps_match_reference_fixture_and_oracle(golden_dir, dp_inline):
+    """The inline-step form (csrc/dp.hip "Inline steps") gives the pipeline's
+    results exactly: PHP(6,5) against the reference's own run, step by step
+    (recording runs one step per slot, inline when it fits) and unrecorded
+    (many inline steps per slot, the assembly of large ones handed to the
+    pipeline's assemble kernel), and random formulas against the oracle."""
+    with open(os.path.join(golden_dir, "dp_php65.json")) as fh:
+        (c,) = json.load(fh)["cases"]
+    r = eliminate(c["formula"], record=True)
+    assert r["result"] == int(c["result"]) == 0
+    assert r["vars"] == [s["var"] for s in c["steps"]]
+    done = [s for s in c["steps"] if "sha256" in s]
+    for k, s in enumerate(done):
+        assert clause_list_sha(r["clauses"][k]) == s["sha256"], k
+    for _ in range(3):   # the learned slot count and the captured graph replayed
+        r2 = eliminate(c["formula"])
+        assert (r2["result"], r2["vars"]) == (r["result"], r["vars"])
+    rng = random.Random(31)
+    for it in range(60):
+        n = rng.randint(2, 12)
+        m = rng.randint(1, 30)
+        f = [[v if rng.random() < 0.5 else -v for v in rng.sample(range(1, n + 1), rng.randint(1, min(4, n)))]
+             for _ in range(m)]
+        if it % 4 == 1:
+            f = [[x * 37 for x in c] for c in f]
+        o = oracle.dp(f, record=True)
+        r = eliminate(f, record=True, time_limit=60.0)
+        assert (r["result"], r["vars"]) == (o["result"], o["vars"]), f
+        assert r["clauses"] == o["clauses"][:_completed(o)], f
+        r2 = eliminate(f)
+        assert (r2["result"], r2["vars"]) == (o["result"], o["vars"]), f
+    batch = cnf.uniform_ksat(16, 16, 96, 3, seed=7002)   # the bench's rand-dp set
+    for b in range(16):
+        f = batch.instance(b)
+        o = oracle.dp(f)
+        assert (lambda x: (x["result"], x["vars"]))(eliminate(f)) == (o["result"], o["vars"]), b
