@@ -110,8 +110,9 @@ LEGS = [
                                           "--cpu-scaled"]),
     # 5-SAT n=200 decided to the end (alpha 12), split always: a step's time is
     # its hardest search's, so the batch is large (2,048 per step 172/s, 8,192
-    # 354/s, 16,384 565/s: profiles/r06/solved_sweep.txt)
-    ("configs[4] 5sat-n200 solved", "5sat-n200-a12", ["--total", "16384", "--split-always", "--steps", "1",
+    # 354/s, 16,384 565/s: profiles/r06/solved_sweep.txt), two steps so that
+    # one stream's tail overlaps the other's bulk (one step: 347/s)
+    ("configs[4] 5sat-n200 solved", "5sat-n200-a12", ["--total", "16384", "--split-always", "--steps", "2",
                                                      "--warmup", "0", "--cpu-scaled"]),
     ("cdcl", "cdcl", ["--steps", "3", "--warmup", "1"]),
     ("cdcl 4 threads", "cdcl", ["--steps", "3", "--warmup", "1", "--threads", "4"]),
