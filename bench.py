@@ -532,8 +532,16 @@ def run_dpll(args, world, rank, local):
     resident = min(B + extra, ncu * per_cu)
     # NS streams' launches overlap: at most every CU slot busy at once
     resident_all = min(NS * (B + extra), ncu * per_cu)
-    # busy wave-time over resident wave-time of the timed region (all streams)
+    # busy wave-time over resident wave-time of the timed region (all streams);
+    # a splitting launch: each wave's own search time over the launch's waves x
+    # its span, for the last launch of every stream (satmi_dpll_split_busy:
+    # measured per wave, not through the rows a split search's helpers add to)
     util = ticks / world / hz / (resident_all * elapsed)
+    if split_used:
+        last_j = {j % NS: j for j in range(args.steps)}
+        busy = sum(_capi.split_busy(streams[si].cuda_stream) for si in last_j)
+        span_sum = sum(span_ms[j] for j in last_j.values()) * 1e-3
+        util = busy / hz / (resident * span_sum) if span_sum > 0 else None
     pmc = load_profile("pmc_traffic.json", workload)
     kname = dpll_kernel_name(n, m, k, split_used)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -294,6 +294,14 @@ int satmi_dpll_set_split_warmup(int nodes);
  * (out[6] = 0) when that launch did not split. */
 int satmi_dpll_split_stats(void *stream, int64_t *out);
 
+/* Wave ticks (satmi_wallclock_hz) that the waves of the last DPLL launch on
+ * `stream` spent inside searches, summed over the launch's waves, if that
+ * launch split (else 0; waits for the stream).  Divided by the launch's waves
+ * and its span (satmi_dpll_launch_span) it is the launch's wave utilisation,
+ * measured per wave -- independent of how a split search's rows collect their
+ * helpers' ticks. */
+int satmi_dpll_split_busy(void *stream, int64_t *busy_ticks);
+
 /* The launch satmi_dpll_batch_device would make for this batch shape under the
  * current policy: *kernel = SATMI_KERNEL_SCAN or SATMI_KERNEL_GENERAL, LDS
  * bytes per wavefront, and wavefronts resident per CU (LDS and registers). */

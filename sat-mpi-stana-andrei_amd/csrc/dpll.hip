@@ -1181,6 +1181,32 @@ extern "C" int satmi_dpll_split_stats(void *stream, int64_t *out) {
     return SATMI_OK;
 }
 
+extern "C" int satmi_dpll_split_busy(void *stream, int64_t *busy_ticks) {
+    if (!busy_ticks) {
+        set_error("satmi_dpll_split_busy: busy_ticks is NULL");
+        return SATMI_ERR_ARG;
+    }
+    *busy_ticks = 0;
+    int dev = 0;
+    SATMI_HIP(hipGetDevice(&dev));
+    void *head = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_work_mu);
+        if ((int)g_work.size() > dev) {
+            auto it = g_work[dev].split.find((hipStream_t)stream);
+            auto last = g_work[dev].split_last.find((hipStream_t)stream);
+            if (it != g_work[dev].split.end() && last != g_work[dev].split_last.end() && last->second)
+                head = it->second.first;
+        }
+    }
+    if (!head) return SATMI_OK;   // the stream's last launch did not split
+    unsigned char h[SPLIT_HEAD_BYTES];
+    SATMI_HIP(hipStreamSynchronize((hipStream_t)stream));
+    SATMI_HIP(hipMemcpy(h, head, sizeof(h), hipMemcpyDeviceToHost));
+    *busy_ticks = dpll_split_busy(h);
+    return SATMI_OK;
+}
+
 extern "C" int satmi_dpll_set_split(int enable, int helpers_per_cu) {
     if (helpers_per_cu < 0 || helpers_per_cu > 32) {
         set_error("satmi_dpll_set_split: helpers_per_cu must be in [0, 32]");

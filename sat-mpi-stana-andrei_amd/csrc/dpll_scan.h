@@ -55,6 +55,7 @@ int dpll_scan_resident(int max_vars, int max_clauses, int max_clause_len, bool i
 // copy of it: [donations, tickets, claims, reclaims, helpers, handoffs, done].
 constexpr int SPLIT_HEAD_BYTES = 512;
 void dpll_split_decode(const void *head, int64_t out[7]);
+int64_t dpll_split_busy(const void *head);   // wave ticks the launch's waves spent searching
 
 // Launch on L.stream (asynchronous).  The caller has checked eligibility and
 // zeroed *L.work_counter on the stream.

@@ -1085,7 +1085,8 @@ struct SplitCfg {
     int32_t helpers;           //         waves that registered as helpers
     uint32_t claims, reclaims; //         statistics: subtrees run by helpers, taken back by donors
     unsigned long long handoffs;     //   continuations handed to helpers (see "Hand-off")
-    uint32_t pad2[26];
+    unsigned long long busy;         //   wave ticks spent searching (every wave of the launch)
+    uint32_t pad2[24];
     int32_t slot_cap, slot_bytes, dstack_cap;   // line 3: geometry (read only)
     uint32_t epoch;            // launch tag of the slot states (the pool is not cleared between launches)
     int32_t max_helpers;       // waves beyond this count exit when the queue drains (their CU slots go
@@ -1749,6 +1750,7 @@ __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) 
     SplitCfg *const SPL = SPLIT ? A.split : nullptr;
     const int ln = lane_id();
     bool draining = false;   // the instance queue is empty: take donated subtrees
+    uint64_t busy = 0;       // (split form) this wave's ticks inside searches
     for (;;) {
         int b = -1, task = -1;
         if (!draining) {
@@ -1774,13 +1776,16 @@ __device__ void run_queue(const ScanArgs &A, const SLds<K, C> &S, int32_t *dst) 
             task = w.y;
         }
         // wave-uniform (a divergent-looking b costs 64-bit VGPR address math)
+        const uint64_t tb = SPLIT ? __builtin_amdgcn_s_memrealtime() : 0;
         const bool root_done = solve_instance<K, INC, C, SPLIT>(A, S, uniform_i32(b), uniform_i32(task), dst);
+        if (SPLIT) busy += __builtin_amdgcn_s_memrealtime() - tb;
         if (SPL && ln == 0) {
             if (root_done) add_agent((int32_t *)&SPL->done, 1);   // (own, or a donor's handed over)
             if (draining) add_agent(&SPL->want, 1);                // a helper asks for its next subtree
         }
         wave_sync();
     }
+    if (SPL && ln == 0) add_agent(&SPL->busy, (unsigned long long)busy);
 }
 
 // Persistent grid: waves pull instance indices from a global counter until the
@@ -2021,6 +2026,8 @@ void launch_kernel(int K, int lvs, dim3 g, dim3 blk, uint32_t wg_lds, hipStream_
 }
 
 }  // namespace
+
+int64_t dpll_split_busy(const void *head) { return (int64_t)((const SplitCfg *)head)->busy; }
 
 void dpll_split_decode(const void *head, int64_t out[7]) {
     static_assert(SPLIT_HEAD_BYTES == SPLIT_POOL_OFF, "split head");

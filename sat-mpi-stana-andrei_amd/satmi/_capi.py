@@ -33,6 +33,7 @@ EXPORTED = (
     "satmi_dp_last_stats",
     "satmi_cdcl_batch_host", "satmi_dpll_set_split_warmup", "satmi_resolution_debug_cand_bytes",
     "satmi_dp_trim", "satmi_resolution_trim", "satmi_cdcl_last_stats", "satmi_launch_chain_floor",
+    "satmi_dpll_split_busy",
 )
 
 
@@ -68,6 +69,13 @@ def split_stats(stream=None):
     check(load().satmi_dpll_split_stats(stream, out), "satmi_dpll_split_stats")
     keys = ("donations", "tickets", "claims", "reclaims", "helpers", "handoffs", "done")
     return dict(zip(keys, list(out)))
+
+
+def split_busy(stream=None):
+    """Wave ticks the waves of the last split DPLL launch on `stream` spent searching (0: it did not split)."""
+    out = ctypes.c_int64(0)
+    check(load().satmi_dpll_split_busy(stream, ctypes.byref(out)), "satmi_dpll_split_busy")
+    return out.value
 
 
 class SatmiError(RuntimeError):
@@ -110,6 +118,7 @@ def load():
     L.satmi_dpll_set_kernel.argtypes = [ctypes.c_int]
     L.satmi_dpll_set_split.argtypes = [ctypes.c_int, ctypes.c_int]
     L.satmi_dpll_split_stats.argtypes = [vp, i64p]
+    L.satmi_dpll_split_busy.argtypes = [vp, i64p]
     L.satmi_dpll_set_split_warmup.argtypes = [ctypes.c_int]
     L.satmi_dpll_launch_span.argtypes = [vp, vp]
     L.satmi_wallclock_hz.argtypes = [P(ctypes.c_double)]
