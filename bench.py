@@ -75,7 +75,7 @@ FIX_NCAP, FIX_MCAP = 127, 448  # dpll_fixed_kernel's shape class (csrc/dpll_scan
 WORKLOADS = {
     "3sat-n100": (262144, 100, 4.26, 3, 0, "configs[2]"),
     "3sat-n50": (4096, 50, 4.26, 3, 0, "configs[1]"),
-    "uf250": (7680, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 3,840 resident waves (15 / CU)
+    "uf250": (8192, 250, 4.26, 3, 20000, "configs[4]"),        # 2 x the 4,096 resident waves (16 / CU)
     "5sat-n200": (2048, 200, 21.117, 5, 20000, "configs[4]"),  # 2 x the 1,024 resident waves (4 / CU)
     # configs[4]'s 5-SAT n=200 decided to the end: alpha 12 (m=2,400), where
     # every search of a batch finishes (at the threshold none of 64 did in 90 s:

@@ -163,7 +163,9 @@ struct SLds {
     C *fvar;                    // [ncap+1]  decision frames: var | PHASE_BIT once False runs
     C *ftrail;                  // [ncap+1]  trail length before the decision
     C *snap;                    // scratch:  unit-clause snapshot (propagation), entries [0, scap)
-    uint32_t *plist;            // scratch:  pure-literal positions (analysis), aliases snap
+    uint32_t *plist;            // scratch:  pure literals (analysis), aliases snap: their first positions,
+                                //           or (plist_vars) their variables as C, whose positions are
+                                //           S.first[v] - 1
     C *snapg;                   // global:   snapshot entries [scap, m] (16-bit codes only)
     uint32_t scap;
     // incremental kernel only
@@ -195,6 +197,13 @@ __device__ __forceinline__ bool var_free(const uint8_t *lv, uint32_t v) { return
 // by 65,535: dpll_scan_eligible, run_queue), which halves the array --
 // uf250 fits 15 searches per CU instead of 13 (+10 %).  (5-SAT n=200 gains no
 // residency from it and pays the packing's shifts: one word per code there.)
+// The pure-literal list holds variables (16 bits) instead of positions (32)
+// for 3-literal clauses with 16-bit codes: with the snapshot's LDS part at 256
+// entries it halves the wave's scratch, and uf250 fits 16 searches per CU
+// instead of 15 (+10 % node-capped, profiles/r06/uf250_occupancy_ab.txt).
+// (5-SAT n=200 stays at 4 per CU whatever the scratch: positions there.)
+template <int K, typename C>
+constexpr bool plist_vars() { return sizeof(C) == 2 && K == 3; }
 template <int K, typename C>
 constexpr bool cnt_packed() {
 #ifdef SATMI_CNT_PACK_ALL   // A/B variant: byte codes (the bench kernel) packed too
@@ -887,7 +896,11 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
             const uint32_t f = v <= n ? S.first[v] : 0u;
             const bool pure = f != 0u;
             const uint64_t mk = __ballot(pure);
-            if (pure) S.plist[k + __popcll(mk & lt)] = f - 1u;
+            if constexpr (!plist_vars<K, C>()) {
+                if (pure) S.plist[k + __popcll(mk & lt)] = f - 1u;
+            } else {
+                if (pure) ((C *)S.plist)[k + __popcll(mk & lt)] = (C)v;
+            }
             k += __popcll(mk);
         };
         if constexpr (sizeof(C) == 1) {
@@ -913,11 +926,16 @@ __device__ Choice choose(const SLds<K, C> &S, int n, int mpad) {
 template <int K, typename C>
 __device__ int assign_pures(const SLds<K, C> &S, int npure, int tl) {
     const int ln = lane_id();
+    // entry j's first position
+    const auto pos = [&](int j) -> uint32_t {
+        if constexpr (!plist_vars<K, C>()) return S.plist[j];
+        else return S.first[((const C *)S.plist)[j]] - 1u;
+    };
     for (int i0 = 0; i0 < npure; i0 += 64) {
         const int i = i0 + ln;
-        const uint32_t my = i < npure ? S.plist[i] : NONE32;
+        const uint32_t my = i < npure ? pos(i) : NONE32;
         int rank = 0;
-        for (int j = 0; j < npure; ++j) rank += S.plist[j] < my ? 1 : 0;
+        for (int j = 0; j < npure; ++j) rank += pos(j) < my ? 1 : 0;
         if (i < npure) {
             const uint32_t code = field<K>(S.cls[my >> 3], (int)(my & 7u));
             S.trail[tl + rank] = (C)code;
@@ -1894,7 +1912,10 @@ uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
 // snapshot entries kept in LDS: all with byte codes, at most 512 with 16-bit
 // codes (the rest in HBM: snap_put); M = clauses + 1
-uint32_t snap_lds_entries(uint32_t cb, uint32_t M) { return cb == 1 ? M : std::min(M, 512u); }
+// snapshot entries in LDS: all (byte codes), else the first 256 for 3-literal
+// clauses (see plist_vars) and 512 for longer ones (rounds find tens of
+// units; a larger snapshot's tail goes to the wave's HBM scratch)
+uint32_t snap_lds_entries(int K, uint32_t cb, uint32_t M) { return cb == 1 ? M : std::min(M, K == 3 ? 256u : 512u); }
 
 int pick_k(int max_vars, int max_clause_len) {
     if (max_clause_len < 1 || max_clause_len > 5) return 0;
@@ -1922,7 +1943,8 @@ bool make_layout(int K, int max_vars, int max_clauses, bool with_lv, bool inc, u
     lay->trail = o;   o = align16(o + cb * N);
     lay->fvar = o;    o = align16(o + cb * N);
     lay->ftrail = o;  o = align16(o + cb * N);
-    lay->scratch = o; o = align16(o + std::max(cb * snap_lds_entries(cb, M), 4 * N));
+    // the snapshot, or the pure literals (positions, 4 B; variables, cb B: plist_vars)
+    lay->scratch = o; o = align16(o + std::max(cb * snap_lds_entries(K, cb, M), (cb == 2 && K == 3 ? cb : 4u) * N));
     lay->occ_off = o; o = align16(o + (inc ? 2 * (2 * N + 1) : 0u));
     lay->bm = o;      o = align16(o + (inc ? 8 * NW : 0u));
     lay->bytes = o;
@@ -2099,7 +2121,7 @@ int dpll_scan_launch(const ScanLaunch &L) {
     A.occ = nullptr;
     A.occ_cap = 0;
     A.occ_lists = 0;
-    A.snap_lds = P.fixed ? 0u : snap_lds_entries(P.lvs == 256 ? 1u : 2u, (uint32_t)lay.mcap + 1u);
+    A.snap_lds = P.fixed ? 0u : snap_lds_entries(K, P.lvs == 256 ? 1u : 2u, (uint32_t)lay.mcap + 1u);
     A.lay = lay;
     A.split = nullptr;
     // split only where the launch's tail matters: at most SPLIT_MAX_PER_WAVE

@@ -64,10 +64,11 @@ def test_scan_kernel_eligibility_query():
         _capi.set_kernel(_capi.KERNEL_AUTO)
     # the launch's real per-wave LDS: one-wave workgroups keep the literal states
     # in a 256-B static array instead of the image's 2(n+1) = 202 B (+ alignment),
-    # (n <= 127) byte-wide trail / frames / snapshot: 3 x (208 - 112) + (864 - 432),
-    # and one counter word per literal code (816 B) where the 16-bit-code layout
-    # of satmi_dpll_scan_lds_bytes packs two per word (416 B)
-    assert kern == _capi.KERNEL_SCAN and s100 - 208 + 256 - 3 * 96 - 432 + (816 - 416) == lds
+    # (n <= 127) byte-wide trail / frames / snapshot: 3 x (208 - 112) + (512 - 432)
+    # (16-bit codes keep 256 snapshot entries in LDS, byte codes all 427), and one
+    # counter word per literal code (816 B) where the 16-bit-code layout of
+    # satmi_dpll_scan_lds_bytes packs two per word (416 B)
+    assert kern == _capi.KERNEL_SCAN and s100 - 208 + 256 - 3 * 96 - (512 - 432) + (816 - 416) == lds
     # the bench class (K=3, n <= 127, m <= 448) runs the static-layout incremental
     # kernel: 5,108 B per wave whatever the instance size, 32 waves per CU
     assert lds_inc == 5108 and _capi.plan(50, 213, 639, 3)[1] == 5108
