@@ -195,7 +195,7 @@ __device__ __forceinline__ int block_max(int x, int *wsum) {
 // The visiting order of `{abs(lit) for clause in clauses for lit in clause}`
 // (REF.py:100/:128): clause t's table slot i is position (t << 32 | i).  The
 // first position of every variable is an atomicMin, reduced in LDS per block
-// when the variables fit.
+// when the variables fit (lfp: the block's LDS table, used iff A.V <= FP_LDS).
 constexpr int FP_LDS = 2048;
 __device__ __forceinline__ void firstpos_clause(const DpArgs &A, unsigned long long *lfp, const int32_t *t, int64_t mask,
                                                 int64_t c) {
@@ -204,7 +204,7 @@ __device__ __forceinline__ void firstpos_clause(const DpArgs &A, unsigned long l
         if (k == PY_EMPTY || k == PY_DUMMY) continue;
         const int d = A.v2d[k < 0 ? -k : k];
         const unsigned long long pos = ((unsigned long long)c << 32) | (unsigned long long)i;
-        if (lfp)
+        if (A.V <= FP_LDS)
             atomicMin(&lfp[d], pos);
         else
             atomicMin(&A.firstpos[d], pos);
@@ -226,7 +226,7 @@ __device__ __forceinline__ void firstpos_flush(const DpArgs &A, unsigned long lo
 __global__ void __launch_bounds__(256) dp_encode_kernel(DpArgs A, int nclauses, const int32_t *off,
                                                         const int32_t *lits, int64_t cap) {
     __shared__ unsigned long long lfp_sh[FP_LDS];
-    unsigned long long *lfp = A.V <= FP_LDS ? lfp_sh : nullptr;
+    unsigned long long *lfp = lfp_sh;   // used when A.V <= FP_LDS (an LDS pointer: ds_* atomics)
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->t0 = __builtin_amdgcn_s_memrealtime();
     firstpos_begin(A, lfp);
     const ClauseList L = A.g[0];
@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(256) dp_encode_kernel(DpArgs A, int nclauses, 
 // the first-position table of g[cur] from scratch (a resumed solve)
 __global__ void __launch_bounds__(256) dp_firstpos_kernel(DpArgs A) {
     __shared__ unsigned long long lfp_sh[FP_LDS];
-    unsigned long long *lfp = A.V <= FP_LDS ? lfp_sh : nullptr;
+    unsigned long long *lfp = lfp_sh;   // used when A.V <= FP_LDS (an LDS pointer: ds_* atomics)
     firstpos_begin(A, lfp);
     const DpState *S = A.st;
     const ClauseList L = A.g[S->cur];
@@ -1278,18 +1278,43 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
 // clause of the next list.  A rem clause keeps its image; kept resolvent k =
 // pair (i, j) gets the image of (pc - {var}) | (nc - {-var}) (REF.py:114),
 // built by lane 0 -- CPython's insertions are a serial chain of dependent
-// probes -- in the wave's LDS scratch when the step's capacities fit it (else
-// in HBM scratch), then copied to the arena at arena_base + 2*capR*k by the
-// whole wave.  The lanes then read the clause's table slots at once for the
-// next step's first-position table.
-constexpr int ASM_WAVES = 4, ASM_SCRATCH = 1024;   // per wave: int32 slots of AX, BY and R tables
+// probes -- then copied to the arena at arena_base + 2*capR*k by the whole
+// wave.  When the step's capacities fit the wave's LDS scratch, the chain runs
+// on LDS only: the wave first copies pc's and nc's images there (one parallel
+// read each), so every probe of the chain is an LDS round trip, not an L2 one;
+// else the tables are built in HBM scratch.  (A form running the chain on
+// tables held across the wave's registers, a probe a readlane, measured 2x
+// slower: the inlined chains left the kernel SGPR-starved.)  The lanes then
+// read the clause's table slots at once for the next step's first positions.
+constexpr int ASM_WAVES = 4, ASM_SCRATCH = 2048;   // per wave: int32 slots of AX, BY, R and the two sources
+
+// lane 0's chain: ax = a - {var}, by = b - {-var}, r = ax | by, tables at xa /
+// xb / ra (2*cap slots each: the table and its resize spare)
+__device__ __forceinline__ void asm_build(const DView &a, const DView &b, int32_t var, int32_t *xa, int32_t *xb,
+                                          int32_t *ra, int64_t capA, int64_t capB, int64_t capR, DpState *S,
+                                          int64_t &rm, int64_t &rf, int64_t &ru, int64_t &roff) {
+    DSet ax, by, r;
+    dset_init(ax, xa, xa + capA, capA);
+    py_difference1(ax, a, var);    // pc - {var}
+    dset_init(by, xb, xb + capB, capB);
+    py_difference1(by, b, -var);   // nc - {-var}
+    dset_init(r, ra, ra + capR, capR);
+    py_merge(r, dset_view(ax));   // set_copy(AX)
+    py_merge(r, dset_view(by));   // |= BY
+    if (ax.overflow || by.overflow || r.overflow) S->set_ovf = 1;
+    rm = r.mask;
+    rf = r.fill;
+    ru = r.used;
+    roff = r.t - ra;
+}
+
 __global__ void __launch_bounds__(64 * ASM_WAVES) dp_assemble_kernel(DpArgs A) {
     __shared__ unsigned long long lfp_sh[FP_LDS];
     __shared__ int32_t scratch_sh[ASM_WAVES][ASM_SCRATCH];
     DpState *S = A.st;
     if (S->done) return;
     if (S->skip == 1) return;   // (2: an inline step left this kernel its assembly)
-    unsigned long long *lfp = A.V <= FP_LDS ? lfp_sh : nullptr;
+    unsigned long long *lfp = lfp_sh;   // used when A.V <= FP_LDS (an LDS pointer: ds_* atomics)
     firstpos_begin(A, lfp);
     const int cur = S->cur;
     const ClauseList L = A.g[cur], O = A.g[cur ^ 1];
@@ -1297,14 +1322,29 @@ __global__ void __launch_bounds__(64 * ASM_WAVES) dp_assemble_kernel(DpArgs A) {
     const int64_t capA = S->capA, capB = S->capB, capR = S->capR;
     const int32_t var = S->var;
     const int K = A.K, lane = lane_id(), wid = threadIdx.x >> 6;
-    const bool lds_ok = 2 * (capA + capB + capR) <= ASM_SCRATCH;
+    const int64_t tab = 2 * (capA + capB + capR);   // the three tables' slots
+    const bool lds_ok = tab <= ASM_SCRATCH;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < ncl2; t += nwaves) {
-        const int32_t *img;
-        int64_t mask;
+    // (t is wave-uniform: one clause per wavefront)
+    const int64_t t0 = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    for (int64_t t = t0; t < ncl2; t += nwaves) {
+        // first positions (REF.py:128's comprehension order) of clause t's
+        // table, called where the table's address space is known
+        const auto first_positions = [&](const int32_t *img, int64_t mask) {
+            for (int64_t x = lane; x <= mask; x += 64) {
+                const int32_t key = img[x];
+                if (key == PY_EMPTY || key == PY_DUMMY) continue;
+                const int d = A.v2d[key < 0 ? -key : key];
+                const unsigned long long pos = ((unsigned long long)t << 32) | (unsigned long long)x;
+                if (A.V <= FP_LDS)
+                    atomicMin(&lfp[d], pos);
+                else
+                    atomicMin(&A.firstpos[d], pos);
+            }
+        };
         if (t < nr) {
             const int64_t c = A.rlist[t];
-            mask = L.mask[c];
+            const int64_t mask = L.mask[c];
             if (lane == 0) {
                 O.off[t] = L.off[c];
                 O.mask[t] = (int32_t)mask;
@@ -1312,40 +1352,48 @@ __global__ void __launch_bounds__(64 * ASM_WAVES) dp_assemble_kernel(DpArgs A) {
                 O.used[t] = L.used[c];
             }
             if (lane < K) O.bits[t * K + lane] = L.bits[c * K + lane];
-            img = A.arena + L.off[c];
+            first_positions(A.arena + L.off[c], mask);
         } else {
             const int64_t k = t - nr;
             const uint32_t p = A.klist[k];
-            int32_t *xa = lds_ok ? scratch_sh[wid] : A.xs + k * 2 * (capA + capB);
-            int32_t *xb = xa + 2 * capA;
+            const uint32_t i = p / (uint32_t)nn, j = p - i * (uint32_t)nn;
+            const DView va = cl_view(L, A.arena, A.plist[i]), vb = cl_view(L, A.arena, A.nlist[j]);
             int32_t *dst = A.arena + base + k * 2 * capR;
-            int32_t *ra = lds_ok ? xb + 2 * capB : dst;
             int64_t rm = 0, rf = 0, ru = 0, roff = 0;
-            if (lane == 0) {
-                const uint32_t i = p / (uint32_t)nn, j = p - i * (uint32_t)nn;
-                DSet ax, by, r;
-                dset_init(ax, xa, xa + capA, capA);
-                py_difference1(ax, cl_view(L, A.arena, A.plist[i]), var);    // pc - {var}
-                dset_init(by, xb, xb + capB, capB);
-                py_difference1(by, cl_view(L, A.arena, A.nlist[j]), -var);   // nc - {-var}
-                dset_init(r, ra, ra + capR, capR);
-                py_merge(r, dset_view(ax));   // set_copy(AX)
-                py_merge(r, dset_view(by));   // |= BY
-                if (ax.overflow || by.overflow || r.overflow) S->set_ovf = 1;
-                rm = r.mask;
-                rf = r.fill;
-                ru = r.used;
-                roff = r.t - ra;
-            }
-            wave_sync();
-            rm = __shfl(rm, 0);
-            rf = __shfl(rf, 0);
-            ru = __shfl(ru, 0);
-            roff = __shfl(roff, 0);
-            const int32_t *src = ra + roff;
-            int32_t *out = lds_ok ? dst : ra + roff;
-            if (lds_ok)
+            int32_t *out;
+            if (lds_ok) {
+                int32_t *xa = scratch_sh[wid], *xb = xa + 2 * capA, *ra = xb + 2 * capB;
+                if (tab + va.mask + vb.mask + 2 <= ASM_SCRATCH) {   // the sources too: an LDS-only chain
+                    int32_t *ca = scratch_sh[wid] + tab, *cb = ca + va.mask + 1;
+                    for (int64_t x = lane; x <= va.mask; x += 64) ca[x] = va.t[x];
+                    for (int64_t x = lane; x <= vb.mask; x += 64) cb[x] = vb.t[x];
+                    wave_sync();
+                    if (lane == 0)
+                        asm_build({ca, va.mask, va.fill, va.used}, {cb, vb.mask, vb.fill, vb.used}, var, xa, xb, ra,
+                                  capA, capB, capR, S, rm, rf, ru, roff);
+                } else if (lane == 0) {
+                    asm_build(va, vb, var, xa, xb, ra, capA, capB, capR, S, rm, rf, ru, roff);
+                }
+                wave_sync();
+                rm = __shfl(rm, 0);
+                rf = __shfl(rf, 0);
+                ru = __shfl(ru, 0);
+                roff = __shfl(roff, 0);
+                const int32_t *src = ra + roff;
                 for (int64_t x = lane; x <= rm; x += 64) dst[x] = src[x];
+                out = dst;
+                first_positions(src, rm);
+            } else {
+                int32_t *xa = A.xs + k * 2 * (capA + capB), *xb = xa + 2 * capA;
+                if (lane == 0) asm_build(va, vb, var, xa, xb, dst, capA, capB, capR, S, rm, rf, ru, roff);
+                wave_sync();
+                rm = __shfl(rm, 0);
+                rf = __shfl(rf, 0);
+                ru = __shfl(ru, 0);
+                roff = __shfl(roff, 0);
+                out = dst + roff;
+                first_positions(out, rm);
+            }
             if (lane == 0) {
                 O.off[t] = out - A.arena;
                 O.mask[t] = (int32_t)rm;
@@ -1353,18 +1401,6 @@ __global__ void __launch_bounds__(64 * ASM_WAVES) dp_assemble_kernel(DpArgs A) {
                 O.used[t] = (int32_t)ru;
             }
             if (lane < K) O.bits[t * K + lane] = A.rbits[(uint64_t)p * K + lane];
-            img = src;
-            mask = rm;
-        }
-        for (int64_t x = lane; x <= mask; x += 64) {   // first positions (REF.py:128's comprehension order)
-            const int32_t key = img[x];
-            if (key == PY_EMPTY || key == PY_DUMMY) continue;
-            const int d = A.v2d[key < 0 ? -key : key];
-            const unsigned long long pos = ((unsigned long long)t << 32) | (unsigned long long)x;
-            if (lfp)
-                atomicMin(&lfp[d], pos);
-            else
-                atomicMin(&A.firstpos[d], pos);
         }
         wave_sync();   // the wave's scratch is rewritten by its next clause
     }

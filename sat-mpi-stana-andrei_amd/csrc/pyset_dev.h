@@ -15,6 +15,13 @@
 // table-copy and insert-clean fast paths), set_difference (copy-and-discard
 // when len(a) >> 2 > len(b)), set_lookkey / set_discard_entry and set_pop.
 // int hash: hash(k) = k, except hash(-1) == -2.
+//
+// Everything is inlined, so a caller whose tables are all in LDS gets ds_*
+// accesses.  A table is scanned PY_BATCH slots at a time (the slots read
+// together, then processed): the chain of one set operation is a series of
+// dependent round trips, and a scan slot's read does not depend on the adds
+// before it (it reads another table), so batching takes most scan reads off
+// the chain.  Table sizes are powers of two >= PY_MINSIZE = PY_BATCH.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,6 +33,7 @@ constexpr int32_t PY_DUMMY = INT32_MIN;
 constexpr int PY_MINSIZE = 8;
 constexpr int PY_LINEAR_PROBES = 9;
 constexpr int PY_PERTURB_SHIFT = 5;
+constexpr int PY_BATCH = 8;
 
 __host__ __device__ __forceinline__ int64_t py_hash(int32_t k) { return k == -1 ? -2 : (int64_t)k; }
 
@@ -75,7 +83,7 @@ __host__ __device__ __forceinline__ int64_t py_size_after(int64_t n) {
     }
 }
 
-__device__ void py_insert_clean(int32_t *table, uint64_t mask, int32_t key) {
+__device__ __forceinline__ void py_insert_clean(int32_t *table, uint64_t mask, int32_t key) {
     const int64_t h = py_hash(key);
     uint64_t perturb = (uint64_t)h;
     uint64_t i = (uint64_t)h & mask;
@@ -98,7 +106,7 @@ __device__ void py_insert_clean(int32_t *table, uint64_t mask, int32_t key) {
 }
 
 // set_table_resize(so, minused)
-__device__ void py_resize(DSet &s, int64_t minused) {
+__device__ __forceinline__ void py_resize(DSet &s, int64_t minused) {
     int64_t newsize = PY_MINSIZE;
     while (newsize <= minused) newsize <<= 1;
     if (newsize == PY_MINSIZE && s.mask == PY_MINSIZE - 1 && s.fill == s.used) return;   // small table, no dummies
@@ -108,9 +116,13 @@ __device__ void py_resize(DSet &s, int64_t minused) {
     }
     int32_t *nt = s.spare;
     for (int64_t i = 0; i < newsize; ++i) nt[i] = PY_EMPTY;
-    for (int64_t i = 0; i <= s.mask; ++i) {
-        const int32_t k = s.t[i];
-        if (k != PY_EMPTY && k != PY_DUMMY) py_insert_clean(nt, (uint64_t)(newsize - 1), k);
+    for (int64_t i0 = 0; i0 <= s.mask; i0 += PY_BATCH) {
+        int32_t kb[PY_BATCH];
+#pragma unroll
+        for (int j = 0; j < PY_BATCH; ++j) kb[j] = s.t[i0 + j];
+#pragma unroll
+        for (int j = 0; j < PY_BATCH; ++j)
+            if (kb[j] != PY_EMPTY && kb[j] != PY_DUMMY) py_insert_clean(nt, (uint64_t)(newsize - 1), kb[j]);
     }
     s.spare = s.t;
     s.t = nt;
@@ -119,7 +131,7 @@ __device__ void py_resize(DSet &s, int64_t minused) {
 }
 
 // set_add_entry(so, key, hash)
-__device__ void py_add(DSet &s, int32_t key) {
+__device__ __forceinline__ void py_add(DSet &s, int32_t key) {
     if (s.overflow) return;
     const int64_t h = py_hash(key);
     const uint64_t mask = (uint64_t)s.mask;
@@ -169,7 +181,7 @@ __device__ void py_add(DSet &s, int32_t key) {
 }
 
 // set_lookkey: slot of key or -1
-__device__ int64_t py_find(const DView &s, int32_t key) {
+__device__ __forceinline__ int64_t py_find(const DView &s, int32_t key) {
     const int64_t h = py_hash(key);
     const uint64_t mask = (uint64_t)s.mask;
     uint64_t perturb = (uint64_t)h;
@@ -187,14 +199,20 @@ __device__ int64_t py_find(const DView &s, int32_t key) {
 }
 
 // set_merge(so, other)
-__device__ void py_merge(DSet &s, const DView &o) {
+__device__ __forceinline__ void py_merge(DSet &s, const DView &o) {
     if (s.overflow || o.used == 0) return;
     if ((s.fill + o.used) * 5 >= s.mask * 3) {
         py_resize(s, (s.used + o.used) * 2);
         if (s.overflow) return;
     }
     if (s.fill == 0 && s.mask == o.mask && o.fill == o.used) {   // empty target, same size, no dummies: copy
-        for (int64_t i = 0; i <= o.mask; ++i) s.t[i] = o.t[i];
+        for (int64_t i0 = 0; i0 <= o.mask; i0 += PY_BATCH) {
+            int32_t kb[PY_BATCH];
+#pragma unroll
+            for (int j = 0; j < PY_BATCH; ++j) kb[j] = o.t[i0 + j];
+#pragma unroll
+            for (int j = 0; j < PY_BATCH; ++j) s.t[i0 + j] = kb[j];
+        }
         s.fill = o.fill;
         s.used = o.used;
         return;
@@ -202,20 +220,28 @@ __device__ void py_merge(DSet &s, const DView &o) {
     if (s.fill == 0) {   // empty target: insert_clean
         s.fill = o.used;
         s.used = o.used;
-        for (int64_t i = 0; i <= o.mask; ++i) {
-            const int32_t k = o.t[i];
-            if (k != PY_EMPTY && k != PY_DUMMY) py_insert_clean(s.t, (uint64_t)s.mask, k);
+        for (int64_t i0 = 0; i0 <= o.mask; i0 += PY_BATCH) {
+            int32_t kb[PY_BATCH];
+#pragma unroll
+            for (int j = 0; j < PY_BATCH; ++j) kb[j] = o.t[i0 + j];
+#pragma unroll
+            for (int j = 0; j < PY_BATCH; ++j)
+                if (kb[j] != PY_EMPTY && kb[j] != PY_DUMMY) py_insert_clean(s.t, (uint64_t)s.mask, kb[j]);
         }
         return;
     }
-    for (int64_t i = 0; i <= o.mask; ++i) {
-        const int32_t k = o.t[i];
-        if (k != PY_EMPTY && k != PY_DUMMY) py_add(s, k);
+    for (int64_t i0 = 0; i0 <= o.mask; i0 += PY_BATCH) {
+        int32_t kb[PY_BATCH];
+#pragma unroll
+        for (int j = 0; j < PY_BATCH; ++j) kb[j] = o.t[i0 + j];
+#pragma unroll
+        for (int j = 0; j < PY_BATCH; ++j)
+            if (kb[j] != PY_EMPTY && kb[j] != PY_DUMMY) py_add(s, kb[j]);
     }
 }
 
 // dst = a - {key}   (set_difference with a one-element right operand)
-__device__ void py_difference1(DSet &dst, const DView &a, int32_t key) {
+__device__ __forceinline__ void py_difference1(DSet &dst, const DView &a, int32_t key) {
     if ((a.used >> 2) > 1) {   // set_copy_and_difference: copy, then discard -> dummy
         py_merge(dst, a);
         if (dst.overflow) return;
@@ -226,9 +252,13 @@ __device__ void py_difference1(DSet &dst, const DView &a, int32_t key) {
         }
         return;
     }
-    for (int64_t i = 0; i <= a.mask; ++i) {
-        const int32_t k = a.t[i];
-        if (k != PY_EMPTY && k != PY_DUMMY && k != key) py_add(dst, k);
+    for (int64_t i0 = 0; i0 <= a.mask; i0 += PY_BATCH) {
+        int32_t kb[PY_BATCH];
+#pragma unroll
+        for (int j = 0; j < PY_BATCH; ++j) kb[j] = a.t[i0 + j];
+#pragma unroll
+        for (int j = 0; j < PY_BATCH; ++j)
+            if (kb[j] != PY_EMPTY && kb[j] != PY_DUMMY && kb[j] != key) py_add(dst, kb[j]);
     }
 }
 
