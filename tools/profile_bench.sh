@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 ROOT=$(pwd)
 export TMPDIR=/tmp
-timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 600 python bench.py --full-json "$OUT/bench_full.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace" -o trace \
     -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-legs > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$ROOT/$OUT/fetch" -o fetch \
