@@ -1118,8 +1118,13 @@ constexpr int SPLIT_POOL_OFF = 512;
 static_assert(sizeof(SplitCfg) == SPLIT_POOL_OFF, "SplitCfg layout");
 // A donation check every SPLIT_CHECK_NODES nodes, run from the node loop's
 // existing event test (next_event), so the split form's loop carries no
-// per-decision counter: what it keeps live is only read at the checks.
-constexpr uint32_t SPLIT_CHECK_NODES = 16u;
+// per-decision counter: what it keeps live is only read at the checks.  (r06:
+// 16 -> 64 nodes, the N=8 shard +1.5 %, the split form at full size +0.5 %:
+// each check is two dependent agent-scope loads; 256 measured the same as 64.)
+#ifndef SATMI_SPLIT_CHECK_NODES
+#define SATMI_SPLIT_CHECK_NODES 64u
+#endif
+constexpr uint32_t SPLIT_CHECK_NODES = SATMI_SPLIT_CHECK_NODES;
 constexpr int SPLIT_MAX_PER_WAVE = 8;   // split a launch only up to this many instances per resident wave (r06: every
                                          // rank's shard at N=8 / 4 / 2, profiles/r06/slices.json)
 // Kernels come in two forms: SPLIT = false has no branch-splitting code at all
@@ -1425,7 +1430,6 @@ __device__ bool solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     int nu = 0;
     bool dec_round = false;
     int nd = 0;                    // live entries of the donation stack
-    uint32_t nchk = 0;             // donation checks so far
     // the row's tick count collects helpers' busy time minus time spent waiting
     // on them; the wave's own elapsed time is added at the end
     if (SPL && ln == 0) st_agent(&ctr[SATMI_CTR_TICKS], (int64_t)0);
@@ -1617,13 +1621,14 @@ __device__ bool solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
             if (SPL) {
                 // between nodes every decision frame below depth is complete,
                 // so the shallowest open one can be donated here
-                ++nchk;
                 if (is_task && uniform_u32(ld_agent(&slot_ref(A, task).f->cancel))) {
                     status = SATMI_DPLL_TIMEOUT;               // abandoned: the donor found its model first
                     state = ST_DONE;
                     continue;
                 }
-                if (nchk * SPLIT_CHECK_NODES >= SPL->warm && uniform_i32(ld_agent(&SPL->want)) > 0)
+                // warm: this search's nodes so far (c counts since the last flush, and a
+                // flush comes only after far more nodes than any warm-up)
+                if ((flushed || c.nodes >= SPL->warm) && uniform_i32(ld_agent(&SPL->want)) > 0)
                     try_donate<K>(A, S, depth, b, dst, nd);
             }
             if (!SPL || c.nodes >= next_flush) {
@@ -1722,6 +1727,13 @@ __device__ bool solve_instance(const ScanArgs &A, const SLds<K, C> &S, int b, in
     }
     return false;
     }
+}
+
+// The launch's split header (counters zeroed, geometry set) from `cfg`.
+__global__ void __launch_bounds__(64) split_init_kernel(SplitCfg *dst, SplitCfg cfg) {
+    static_assert(sizeof(SplitCfg) % 4 == 0, "SplitCfg words");
+    const uint32_t *src = (const uint32_t *)&cfg;
+    for (int i = threadIdx.x; i < (int)(sizeof(SplitCfg) / 4); i += 64) ((uint32_t *)dst)[i] = src[i];
 }
 
 // An idle wave's next donated subtree: {instance, slot}, or y < 0 once every
@@ -2170,8 +2182,13 @@ int dpll_scan_launch(const ScanLaunch &L) {
             return SATMI_ERR_NOMEM;
         }
         cfg.epoch = epoch & 0x0FFFFFFFu;
-        // pageable source: staged before the call returns
-        SATMI_HIP(hipMemcpyAsync(p, &cfg, sizeof(cfg), hipMemcpyHostToDevice, L.stream));
+        // written by a one-wave kernel on the launch's stream, the header by
+        // value in its arguments: a copy from this pageable host struct would
+        // make the runtime stage it synchronously, and the host then waits for
+        // the stream's earlier work before it can queue the next launch -- the
+        // two-stream overlap of the bench's steps was lost that way (split
+        // form at full size: launch +1 %, step rate -5 %)
+        hipLaunchKernelGGL(split_init_kernel, dim3(1), dim3(64), 0, L.stream, (SplitCfg *)p, cfg);
         A.split = (SplitCfg *)p;
     }
     // per resident wave: occurrence lists (max_lits entries, rounded to 128 B),
