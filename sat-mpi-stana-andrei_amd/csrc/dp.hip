@@ -993,6 +993,10 @@ struct KeyReg {
 };
 
 constexpr int TEST_TILE = 256;
+#ifndef DP_TEST_STEP
+#define DP_TEST_STEP 16   // candidates per step of the test loop (a multiple of 4 dividing TEST_TILE)
+#endif
+static_assert(DP_TEST_STEP % 4 == 0 && TEST_TILE % DP_TEST_STEP == 0, "DP_TEST_STEP");
 
 template <int KT>
 __device__ __forceinline__ bool subset_of(const uint64_t *y, const KeyReg<KT> &x, const uint64_t *xg, int K) {
@@ -1015,8 +1019,8 @@ template <int KT, bool SURV>
 __device__ __forceinline__ void dp_test_items(const DpArgs &A, int64_t nx, int64_t ny, const uint64_t *xkeys,
                                               const uint64_t *ykeys, const uint32_t *ypair, int32_t *stamp,
                                               int32_t epoch, int &tests) {
-    __shared__ uint64_t tile[TEST_TILE * (KT ? KT : 1)];
-    __shared__ uint32_t tp[TEST_TILE];
+    __shared__ __attribute__((aligned(16))) uint64_t tile[TEST_TILE * (KT ? KT : 1)];
+    __shared__ __attribute__((aligned(16))) uint32_t tp[TEST_TILE];
     const int K = A.K, tid = threadIdx.x;
     const int64_t ntx = (nx + TEST_TILE - 1) / TEST_TILE, nty = (ny + TEST_TILE - 1) / TEST_TILE;
     for (int64_t item = blockIdx.x; item < ntx * nty; item += gridDim.x) {
@@ -1042,7 +1046,53 @@ __device__ __forceinline__ void dp_test_items(const DpArgs &A, int64_t nx, int64
                 if (SURV) tp[tid] = ypair[e0 + tid];
             }
             __syncthreads();
-            if (alive) {
+            if (alive && KT > 0) {
+                // DP_TEST_STEP candidates per step, every LDS read of the step
+                // issued before any test (their pair indices as 16-B reads): the
+                // tests are branch-free, so no read waits on an earlier read's
+                // value (a short-circuit form made each step of four a chain of
+                // 8 dependent LDS round trips)
+                constexpr int KW = KT ? KT : 1, NC = DP_TEST_STEP;
+                int j = 0;
+                for (; j < cnt; j += NC) {
+                    uint32_t tq[NC];
+#pragma unroll
+                    for (int q = 0; q < NC; ++q) tq[q] = 0u;
+                    if constexpr (SURV) {
+#pragma unroll
+                        for (int q = 0; q < NC; q += 4) {
+                            const uint4 t4 = *reinterpret_cast<const uint4 *>(tp + j + q);
+                            tq[q] = t4.x;
+                            tq[q + 1] = t4.y;
+                            tq[q + 2] = t4.z;
+                            tq[q + 3] = t4.w;
+                        }
+                    }
+                    uint64_t y[NC][KW];
+#pragma unroll
+                    for (int q = 0; q < NC; ++q)
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) y[q][w] = tile[(j + q) * KW + w];
+                    // (the reads stay above the tests: the scheduler would otherwise
+                    // sink each one to its test and reuse one register set)
+                    __builtin_amdgcn_sched_barrier(0);
+                    bool hit = false;
+#pragma unroll
+                    for (int q = 0; q < NC; ++q) {
+                        uint64_t out = 0;
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) out |= y[q][w] & ~x.w[w];
+                        const bool okq = (j + q < cnt) & (!SURV | (tq[q] < px));
+                        hit |= okq & (out == 0ull);
+                    }
+                    if (hit) {
+                        __hip_atomic_store(stamp + u, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        j += NC;
+                        break;
+                    }
+                }
+                tests += min(j, cnt);
+            } else if (alive) {   // key width known only at run time: keys read from memory
                 const auto yk = [&](int j) { return KT ? tile + j * (KT ? KT : 1) : ykeys + (e0 + j) * K; };
                 const auto ok = [&](int j) { return j < cnt && (!SURV || tp[j] < px); };
                 int j = 0;
