@@ -1336,7 +1336,10 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
 // tables held across the wave's registers, a probe a readlane, measured 2x
 // slower: the inlined chains left the kernel SGPR-starved.)  The lanes then
 // read the clause's table slots at once for the next step's first positions.
-constexpr int ASM_WAVES = 4, ASM_SCRATCH = 2048;   // per wave: int32 slots of AX, BY, R and the two sources
+#ifndef DP_ASM_SCRATCH
+#define DP_ASM_SCRATCH 2048
+#endif
+constexpr int ASM_WAVES = 4, ASM_SCRATCH = DP_ASM_SCRATCH;   // per wave: int32 slots of AX, BY, R and the two sources
 
 // lane 0's chain: ax = a - {var}, by = b - {-var}, r = ax | by, tables at xa /
 // xb / ra (2*cap slots each: the table and its resize spare)
