@@ -1336,6 +1336,9 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
 // tables held across the wave's registers, a probe a readlane, measured 2x
 // slower: the inlined chains left the kernel SGPR-starved.)  The lanes then
 // read the clause's table slots at once for the next step's first positions.
+#ifndef DP_ASM_WAVE
+#define DP_ASM_WAVE 1   // the chain run by the whole wave (0: by lane 0, the r06 form before)
+#endif
 #ifndef DP_ASM_SCRATCH
 #define DP_ASM_SCRATCH 2048
 #endif
@@ -1355,6 +1358,26 @@ __device__ __forceinline__ void asm_build(const DView &a, const DView &b, int32_
     py_merge(r, dset_view(ax));   // set_copy(AX)
     py_merge(r, dset_view(by));   // |= BY
     if (ax.overflow || by.overflow || r.overflow) S->set_ovf = 1;
+    rm = r.mask;
+    rf = r.fill;
+    ru = r.used;
+    roff = r.t - ra;
+}
+
+// the same chain run by the whole wave (pyset_dev.h wpy_*: a probe run per
+// LDS round trip, scans and copies across the lanes), every table in LDS
+__device__ __forceinline__ void asm_build_wave(const DView &a, const DView &b, int32_t var, int32_t *xa, int32_t *xb,
+                                               int32_t *ra, int64_t capA, int64_t capB, int64_t capR, DpState *S,
+                                               int64_t &rm, int64_t &rf, int64_t &ru, int64_t &roff) {
+    DSet ax, by, r;
+    wdset_init(ax, xa, xa + capA, capA);
+    wpy_difference1(ax, a, var);    // pc - {var}
+    wdset_init(by, xb, xb + capB, capB);
+    wpy_difference1(by, b, -var);   // nc - {-var}
+    wdset_init(r, ra, ra + capR, capR);
+    wpy_merge(r, dset_view(ax));   // set_copy(AX)
+    wpy_merge(r, dset_view(by));   // |= BY
+    if (__lane_id() == 0 && (ax.overflow || by.overflow || r.overflow)) S->set_ovf = 1;
     rm = r.mask;
     rf = r.fill;
     ru = r.used;
@@ -1421,9 +1444,14 @@ __global__ void __launch_bounds__(64 * ASM_WAVES) dp_assemble_kernel(DpArgs A) {
                     for (int64_t x = lane; x <= va.mask; x += 64) ca[x] = va.t[x];
                     for (int64_t x = lane; x <= vb.mask; x += 64) cb[x] = vb.t[x];
                     wave_sync();
+#if DP_ASM_WAVE
+                    asm_build_wave({ca, va.mask, va.fill, va.used}, {cb, vb.mask, vb.fill, vb.used}, var, xa, xb, ra,
+                                   capA, capB, capR, S, rm, rf, ru, roff);
+#else
                     if (lane == 0)
                         asm_build({ca, va.mask, va.fill, va.used}, {cb, vb.mask, vb.fill, vb.used}, var, xa, xb, ra,
                                   capA, capB, capR, S, rm, rf, ru, roff);
+#endif
                 } else if (lane == 0) {
                     asm_build(va, vb, var, xa, xb, ra, capA, capB, capR, S, rm, rf, ru, roff);
                 }

@@ -262,4 +262,197 @@ __device__ __forceinline__ void py_difference1(DSet &dst, const DView &a, int32_
     }
 }
 
+// ---- Wave-cooperative forms, for tables in LDS.  Every lane of a wavefront
+// calls them with the same arguments and keeps the same DSet fields.  A probe
+// run (slot i, and the PY_LINEAR_PROBES after it when they fit) is read at
+// once, one lane per slot, and settled by ballots in probe order -- the result
+// of the serial probe loop above, in one LDS round trip per run instead of one
+// per slot; table clears, copies and scans run across the lanes.  (A wave's
+// LDS accesses complete in order, so a write by one lane is seen by the next
+// read of any lane of the same wave.)
+
+// lanes of the probe run at slot i
+__device__ __forceinline__ uint64_t wpy_run(uint64_t i, uint64_t mask) {
+    return (i + PY_LINEAR_PROBES <= mask) ? ((1ull << (PY_LINEAR_PROBES + 1)) - 1ull) : 1ull;
+}
+
+__device__ __forceinline__ void wpy_clear(int32_t *t, int64_t n) {
+    for (int64_t x = __lane_id(); x < n; x += 64) t[x] = PY_EMPTY;
+}
+
+__device__ __forceinline__ void wpy_insert_clean(int32_t *table, uint64_t mask, int32_t key) {
+    const uint32_t lane = __lane_id();
+    const int64_t h = py_hash(key);
+    uint64_t perturb = (uint64_t)h;
+    uint64_t i = (uint64_t)h & mask;
+    for (;;) {
+        const bool in = (wpy_run(i, mask) >> lane) & 1ull;
+        const int32_t k = in ? table[i + lane] : 1;
+        const uint64_t em = __ballot(in && k == PY_EMPTY);
+        if (em) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(em);
+            if (lane == f) table[i + f] = key;
+            return;
+        }
+        perturb >>= PY_PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+__device__ __forceinline__ void wpy_resize(DSet &s, int64_t minused) {
+    int64_t newsize = PY_MINSIZE;
+    while (newsize <= minused) newsize <<= 1;
+    if (newsize == PY_MINSIZE && s.mask == PY_MINSIZE - 1 && s.fill == s.used) return;   // small table, no dummies
+    if (newsize > s.cap) {
+        s.overflow = true;
+        return;
+    }
+    int32_t *nt = s.spare;
+    wpy_clear(nt, newsize);
+    const uint32_t lane = __lane_id();
+    for (int64_t x0 = 0; x0 <= s.mask; x0 += 64) {   // old members in slot order
+        const int32_t k = x0 + lane <= s.mask ? s.t[x0 + lane] : PY_EMPTY;
+        uint64_t live = __ballot(k != PY_EMPTY && k != PY_DUMMY);
+        while (live) {
+            const int b = __builtin_ctzll(live);
+            live &= live - 1;
+            wpy_insert_clean(nt, (uint64_t)(newsize - 1), __builtin_amdgcn_readlane(k, b));
+        }
+    }
+    s.spare = s.t;
+    s.t = nt;
+    s.mask = newsize - 1;
+    s.fill = s.used;
+}
+
+// set_add_entry, wave-cooperative (see py_add: the LAST dummy before the first
+// empty slot is reused)
+__device__ __forceinline__ void wpy_add(DSet &s, int32_t key) {
+    if (s.overflow) return;
+    const uint32_t lane = __lane_id();
+    const int64_t h = py_hash(key);
+    const uint64_t mask = (uint64_t)s.mask;
+    uint64_t i = (uint64_t)h & mask;
+    uint64_t perturb = (uint64_t)h;
+    int64_t freeslot = -1, slot;
+    for (;;) {
+        const bool in = (wpy_run(i, mask) >> lane) & 1ull;
+        const int32_t k = in ? s.t[i + lane] : 1;
+        const uint64_t em = __ballot(in && k == PY_EMPTY);
+        const uint64_t km = __ballot(in && k == key);
+        const uint64_t dm = __ballot(in && k == PY_DUMMY);
+        const uint64_t stop = em | km;
+        if (stop) {
+            const int f = __builtin_ctzll(stop);
+            if ((km >> f) & 1ull) return;                                   // found_active
+            const uint64_t before = dm & ((1ull << f) - 1ull);
+            if (before) freeslot = (int64_t)(i + 63 - __builtin_clzll(before));
+            slot = (int64_t)(i + f);
+            break;
+        }
+        if (dm) freeslot = (int64_t)(i + 63 - __builtin_clzll(dm));
+        perturb >>= PY_PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+    if (freeslot >= 0) {   // found_unused_or_dummy: a dummy was probed first
+        s.used++;
+        if (lane == 0) s.t[freeslot] = key;
+        return;
+    }
+    s.fill++;   // found_unused
+    s.used++;
+    if (lane == 0) s.t[slot] = key;
+    if ((uint64_t)s.fill * 5 < mask * 3) return;
+    wpy_resize(s, s.used > 50000 ? s.used * 2 : s.used * 4);
+}
+
+__device__ __forceinline__ int64_t wpy_find(const DView &s, int32_t key) {
+    const uint32_t lane = __lane_id();
+    const int64_t h = py_hash(key);
+    const uint64_t mask = (uint64_t)s.mask;
+    uint64_t perturb = (uint64_t)h;
+    uint64_t i = (uint64_t)h & mask;
+    for (;;) {
+        const bool in = (wpy_run(i, mask) >> lane) & 1ull;
+        const int32_t k = in ? s.t[i + lane] : 1;
+        const uint64_t em = __ballot(in && k == PY_EMPTY);
+        const uint64_t km = __ballot(in && k == key);
+        const uint64_t stop = em | km;
+        if (stop) {
+            const int f = __builtin_ctzll(stop);
+            return ((km >> f) & 1ull) ? (int64_t)(i + f) : -1;
+        }
+        perturb >>= PY_PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+__device__ __forceinline__ void wdset_init(DSet &s, int32_t *a, int32_t *b, int64_t cap) {
+    s.t = a;
+    s.spare = b;
+    s.cap = cap;
+    s.mask = PY_MINSIZE - 1;
+    s.fill = s.used = 0;
+    s.overflow = cap < PY_MINSIZE;
+    wpy_clear(a, cap < PY_MINSIZE ? cap : PY_MINSIZE);
+}
+
+// set_merge, wave-cooperative
+__device__ __forceinline__ void wpy_merge(DSet &s, const DView &o) {
+    if (s.overflow || o.used == 0) return;
+    if ((s.fill + o.used) * 5 >= s.mask * 3) {
+        wpy_resize(s, (s.used + o.used) * 2);
+        if (s.overflow) return;
+    }
+    const uint32_t lane = __lane_id();
+    if (s.fill == 0 && s.mask == o.mask && o.fill == o.used) {   // empty target, same size, no dummies: copy
+        for (int64_t x = lane; x <= o.mask; x += 64) s.t[x] = o.t[x];
+        s.fill = o.fill;
+        s.used = o.used;
+        return;
+    }
+    const bool clean = s.fill == 0;   // empty target: insert_clean
+    if (clean) {
+        s.fill = o.used;
+        s.used = o.used;
+    }
+    for (int64_t x0 = 0; x0 <= o.mask; x0 += 64) {   // o's members in slot order
+        const int32_t k = x0 + lane <= o.mask ? o.t[x0 + lane] : PY_EMPTY;
+        uint64_t live = __ballot(k != PY_EMPTY && k != PY_DUMMY);
+        while (live) {
+            const int b = __builtin_ctzll(live);
+            live &= live - 1;
+            const int32_t key = __builtin_amdgcn_readlane(k, b);
+            if (clean)
+                wpy_insert_clean(s.t, (uint64_t)s.mask, key);
+            else
+                wpy_add(s, key);
+        }
+    }
+}
+
+// dst = a - {key}, wave-cooperative
+__device__ __forceinline__ void wpy_difference1(DSet &dst, const DView &a, int32_t key) {
+    if ((a.used >> 2) > 1) {   // set_copy_and_difference: copy, then discard -> dummy
+        wpy_merge(dst, a);
+        if (dst.overflow) return;
+        const int64_t at = wpy_find(dset_view(dst), key);
+        if (at >= 0) {
+            if (__lane_id() == 0) dst.t[at] = PY_DUMMY;
+            dst.used--;
+        }
+        return;
+    }
+    const uint32_t lane = __lane_id();
+    for (int64_t x0 = 0; x0 <= a.mask; x0 += 64) {
+        const int32_t k = x0 + lane <= a.mask ? a.t[x0 + lane] : PY_EMPTY;
+        uint64_t live = __ballot(k != PY_EMPTY && k != PY_DUMMY && k != key);
+        while (live) {
+            const int b = __builtin_ctzll(live);
+            live &= live - 1;
+            wpy_add(dst, __builtin_amdgcn_readlane(k, b));
+        }
+    }
+}
+
 }  // namespace satmi
