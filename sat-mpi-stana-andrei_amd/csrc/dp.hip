@@ -192,6 +192,58 @@ __device__ __forceinline__ int block_max(int x, int *wsum) {
     return r;
 }
 
+// Several block reductions in one LDS exchange (two barriers in all; the
+// single-workgroup kernels are chains of such exchanges).  ws: 16 ints per
+// value (up to 16 waves).
+__device__ __forceinline__ int wave_sum_i32(int x) {
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+// a summed, b and c maxed (all >= 0)
+__device__ __forceinline__ void block_sum_max_max(int &a, int &b, int &c, int *ws) {
+    const int sa = wave_sum_i32(a), mb = wave_max_i32(b), mc = wave_max_i32(c);
+    const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane_id() == 0) {
+        ws[wid] = sa;
+        ws[16 + wid] = mb;
+        ws[32 + wid] = mc;
+    }
+    __syncthreads();
+    int ra = 0, rb = 0, rc = 0;
+    for (int w = 0; w < nw; ++w) {
+        ra += ws[w];
+        rb = max(rb, ws[16 + w]);
+        rc = max(rc, ws[32 + w]);
+    }
+    __syncthreads();
+    a = ra;
+    b = rb;
+    c = rc;
+}
+// exclusive prefix sums of x and y (block totals in tx, ty)
+__device__ __forceinline__ void block_excl_scan2(int &x, int &y, int *ws, int &tx, int &ty) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int ix = wave_incl_scan(x), iy = wave_incl_scan(y);
+    if (lane == 63) {
+        ws[wid] = ix;
+        ws[16 + wid] = iy;
+    }
+    __syncthreads();
+    int ox = 0, oy = 0, sx = 0, sy = 0;
+    for (int w = 0; w < nw; ++w) {
+        const int vx = ws[w], vy = ws[16 + w];
+        ox += w < wid ? vx : 0;
+        oy += w < wid ? vy : 0;
+        sx += vx;
+        sy += vy;
+    }
+    __syncthreads();
+    tx = sx;
+    ty = sy;
+    x = ox + ix - x;
+    y = oy + iy - y;
+}
+
 // The visiting order of `{abs(lit) for clause in clauses for lit in clause}`
 // (REF.py:100/:128): clause t's table slot i is position (t << 32 | i).  The
 // first position of every variable is an atomicMin, reduced in LDS per block
@@ -669,7 +721,7 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
     __shared__ unsigned long long fp_sh[FP_LDS];
     __shared__ int32_t ord_sh[FP_LDS];
     __shared__ int32_t pop_sh[2 * POP_LDS];
-    __shared__ int wsum[16];
+    __shared__ int wsum[48];
     __shared__ int64_t sh_ncl;
     __shared__ int sh_cur, sh_quit, sh_var;
     __shared__ std::conditional_t<INL, InlLds, char> inl;
@@ -708,9 +760,9 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
         vmax = max(vmax, v);
         vlow = max(vlow, INT32_MAX - v);
     }
-    const int nv = block_sum(live, wsum);
-    vmax = block_max(vmax, wsum);
-    const int32_t vmin = INT32_MAX - block_max(vlow, wsum);
+    block_sum_max_max(live, vmax, vlow, wsum);
+    const int nv = live;
+    const int32_t vmin = INT32_MAX - vlow;
     // every variable below the set's final table size: pop() is the smallest
     // (pyset_dev.h py_size_after); otherwise the set is built in insertion order
     const bool small_ints = nv > 0 && (int64_t)vmax < py_size_after(nv);
@@ -781,20 +833,20 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
     for (int64_t c = c0; c < c1; ++c) {
         const bool p = (L.bits[c * K + dw] >> db) & 1ull;
         const bool q = (L.bits[c * K + W + dw] >> db) & 1ull;
+        const int u = L.used[c];   // (read with the flags: no second dependent load)
         if (small) fl |= (p ? 1u : 0u) << (2 * (c - c0)) | (q ? 2u : 0u) << (2 * (c - c0));
         cp += p;
         cq += q;
         cr += !p && !q;
-        if (p | q) {
-            const int u = L.used[c];
-            if (p) mxA = max(mxA, u);
-            if (q) mxB = max(mxB, u);
-        }
+        mxA = p ? max(mxA, u) : mxA;
+        mxB = q ? max(mxB, u) : mxB;
     }
-    int tot, tr, ep, en;
+    int tot, tr, ep, en, er;
     int64_t np, nn;
-    if (ncl < 65536) {   // both counts in one scan (halves < 2^16)
-        const int ex = block_excl_scan(cp | (cq << 16), wsum, tot);
+    if (ncl < 65536) {   // pos and neg counts in one word (halves < 2^16), rem beside them: one exchange
+        int ex = cp | (cq << 16);
+        er = cr;
+        block_excl_scan2(ex, er, wsum, tot, tr);
         ep = ex & 0xFFFF;
         en = ex >> 16;
         np = tot & 0xFFFF;
@@ -803,10 +855,10 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
         int tn;
         ep = block_excl_scan(cp, wsum, tot);
         en = block_excl_scan(cq, wsum, tn);
+        er = block_excl_scan(cr, wsum, tr);
         np = tot;
         nn = tn;
     }
-    int er = block_excl_scan(cr, wsum, tr);
     const int64_t nr = tr;
     for (int64_t c = c0; c < c1; ++c) {   // a clause may be in both the pos and the neg list
         bool p, q;
@@ -824,8 +876,10 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
             A.rlist[er++] = c;
         }
     }
-    mxA = block_max(mxA, wsum);
-    mxB = block_max(mxB, wsum);
+    {
+        int zero = 0;
+        block_sum_max_max(zero, mxA, mxB, wsum);
+    }
     const int64_t npairs = np * nn;
     if (npairs > A.pair_cap) {   // grow the pair buffers and run this step again
         if (tid == 0) {
