@@ -1269,6 +1269,12 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
     if (S->done || S->skip) return;
     const int tid = threadIdx.x;
     const uint64_t fe = S->first_empty;
+    // every state field this kernel reads, up front: one round trip, not one
+    // per phase (a barrier keeps a later load from being hoisted above it);
+    // none of them is written here before it is read
+    const int64_t npairs = S->npairs, nr = S->nr, ns = S->nsurv;
+    const int32_t epoch = S->epoch;
+    const int64_t capA = S->capA, capB = S->capB, capR = S->capR, arena_top = S->arena_top;
     __shared__ int64_t sh_nt;
     if (tid < 64) {   // the striped counters of this step (one wave)
         int64_t nt = (int64_t)A.stripes[DP_STRIPES + tid], ts = (int64_t)A.stripes[2 * DP_STRIPES + tid];
@@ -1283,7 +1289,7 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
         }
     }
     __syncthreads();
-    const int64_t npairs = S->npairs, nr = S->nr, nontaut = sh_nt;
+    const int64_t nontaut = sh_nt;
     // clause_limit: the reference stops when remaining + new passes the limit,
     // i.e. at the kth non-tautological non-empty pair (0-based)
     int64_t limit_pair = -1;
@@ -1320,14 +1326,11 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
         }
         return;
     }
-    const int64_t ns = S->nsurv;
-    const int32_t epoch = S->epoch;
     int kc = 0;
     for (int64_t i = tid; i < ns; i += POP_THREADS) kc += A.hit[i] != epoch ? 1 : 0;
     const int nkept = block_sum(kc, wsum);
     const int64_t ncl2 = nr + nkept;
-    const int64_t capA = S->capA, capB = S->capB, capR = S->capR;
-    const int64_t arena_need = S->arena_top + (int64_t)nkept * 2 * capR;
+    const int64_t arena_need = arena_top + (int64_t)nkept * 2 * capR;
     const int64_t xs_need = (int64_t)nkept * 2 * (capA + capB);
     int ovf = 0;
     if (ncl2 > A.ncl_cap) ovf |= OVF_NCL;
@@ -1371,7 +1374,7 @@ __global__ void __launch_bounds__(POP_THREADS) dp_kept_kernel(DpArgs A) {
     if (tid == 0) {
         S->nkept = nkept;
         S->ncl2 = ncl2;
-        S->arena_base = S->arena_top;
+        S->arena_base = arena_top;
         S->arena_top = arena_need;
         S->new_total += nontaut;
         S->pending = 1;
