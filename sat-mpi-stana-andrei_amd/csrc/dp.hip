@@ -192,6 +192,10 @@ __device__ __forceinline__ int block_max(int x, int *wsum) {
     return r;
 }
 
+// A value loaded before a kernel's early-exit test stays loaded there (the
+// compiler would otherwise sink the load below the test: a second round trip)
+#define DP_KEEP(x) asm volatile("" ::"s"(x))
+
 // Several block reductions in one LDS exchange (two barriers in all; the
 // single-workgroup kernels are chains of such exchanges).  ws: 16 ints per
 // value (up to 16 waves).
@@ -943,11 +947,16 @@ __global__ void __launch_bounds__(POP_THREADS) dp_pop_split_kernel(DpArgs A) {
 __global__ void __launch_bounds__(256) dp_pairs_kernel(DpArgs A) {
     __shared__ int wsum[4];
     DpState *S = A.st;
-    if (S->done) return;
-    if (S->skip) return;
+    // (the state fields loaded together before any test: one round trip, see dp_kept_kernel)
+    const int done = S->done, skip = S->skip, cur = S->cur, d = S->d;
     const uint32_t npairs = (uint32_t)S->npairs, nn = (uint32_t)S->nn;
-    const int d = S->d, W = A.W, K = A.K;
-    const ClauseList L = A.g[S->cur];
+    DP_KEEP(cur);
+    DP_KEEP(d);
+    DP_KEEP(npairs);
+    DP_KEEP(nn);
+    if (done || skip) return;
+    const int W = A.W, K = A.K;
+    const ClauseList L = A.g[cur];
     const uint64_t vb = 1ull << (d & 63);
     const int vw = d >> 6, lane = lane_id();
     int cnt = 0;
@@ -991,8 +1000,11 @@ __device__ __forceinline__ uint64_t dp_mix64(uint64_t z) {
 // claim goes to uslot.
 __global__ void __launch_bounds__(256) dp_hash_kernel(DpArgs A) {
     DpState *S = A.st;
-    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;   // the step ends in an empty clause
+    const int done = S->done, skip = S->skip;
+    const uint64_t fe = S->first_empty;
     const uint32_t npairs = (uint32_t)S->npairs;
+    DP_KEEP(npairs);
+    if (done || skip || fe != DP_EMPTY) return;   // the step ends in an empty clause
     const int K = A.K, lane = lane_id();
     for (uint32_t p0 = blockIdx.x * 256u + (threadIdx.x & ~63u); p0 < npairs; p0 += gridDim.x * 256u) {
         const uint32_t p = p0 + lane;
@@ -1174,9 +1186,16 @@ template <int KT>
 __global__ void __launch_bounds__(TEST_TILE) dp_remtest_kernel(DpArgs A) {
     __shared__ int wsum[4];
     DpState *S = A.st;
-    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;
+    const int done = S->done, skip = S->skip;
+    const uint64_t fe = S->first_empty;
+    const int64_t nuniq = S->nuniq, nr = S->nr;
+    const int32_t epoch = S->epoch;
+    DP_KEEP(nuniq);
+    DP_KEEP(nr);
+    DP_KEEP(epoch);
+    if (done || skip || fe != DP_EMPTY) return;
     int tests = 0;
-    dp_test_items<KT, false>(A, S->nuniq, S->nr, A.ukeys, A.rkeys, nullptr, A.dropped, S->epoch, tests);
+    dp_test_items<KT, false>(A, nuniq, nr, A.ukeys, A.rkeys, nullptr, A.dropped, epoch, tests);
     const int tot = block_sum(tests, wsum);
     if (threadIdx.x == 0 && tot) atomicAdd(A.stripes + 2 * DP_STRIPES + blockIdx.x % DP_STRIPES, (unsigned long long)tot);
 }
@@ -1187,7 +1206,9 @@ __global__ void __launch_bounds__(TEST_TILE) dp_remtest_kernel(DpArgs A) {
 __global__ void __launch_bounds__(256) dp_gather_kernel(DpArgs A) {
     __shared__ int64_t pre[DP_STRIPES + 1];
     DpState *S = A.st;
-    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;
+    const int done = S->done, skip = S->skip;
+    const uint64_t fe = S->first_empty;
+    if (done || skip || fe != DP_EMPTY) return;
     if (threadIdx.x == 0) {
         int64_t acc = 0;
         for (int t = 0; t < DP_STRIPES; ++t) {
@@ -1212,9 +1233,13 @@ __global__ void __launch_bounds__(256) dp_gather_kernel(DpArgs A) {
 // every used table slot cleared for the next step
 __global__ void __launch_bounds__(256) dp_survlist_kernel(DpArgs A) {
     DpState *S = A.st;
-    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;
+    const int done = S->done, skip = S->skip;
+    const uint64_t fe = S->first_empty;
     const int64_t nuniq = S->nuniq;
     const int32_t epoch = S->epoch;
+    DP_KEEP(nuniq);
+    DP_KEEP(epoch);
+    if (done || skip || fe != DP_EMPTY) return;
     const int lane = lane_id(), K = A.K, tid = threadIdx.x;
     __shared__ int wcnt[4];
     __shared__ uint32_t bbase;
@@ -1252,9 +1277,15 @@ template <int KT>
 __global__ void __launch_bounds__(TEST_TILE) dp_survtest_kernel(DpArgs A) {
     __shared__ int wsum[4];
     DpState *S = A.st;
-    if (S->done || S->skip || S->first_empty != DP_EMPTY) return;
+    const int done = S->done, skip = S->skip;
+    const uint64_t fe = S->first_empty;
+    const int64_t nsurv = S->nsurv;
+    const int32_t epoch = S->epoch;
+    DP_KEEP(nsurv);
+    DP_KEEP(epoch);
+    if (done || skip || fe != DP_EMPTY) return;
     int tests = 0;
-    dp_test_items<KT, true>(A, S->nsurv, S->nsurv, A.skeys, A.skeys, A.surv, A.hit, S->epoch, tests);
+    dp_test_items<KT, true>(A, nsurv, nsurv, A.skeys, A.skeys, A.surv, A.hit, epoch, tests);
     const int tot = block_sum(tests, wsum);
     if (threadIdx.x == 0 && tot) atomicAdd(A.stripes + 2 * DP_STRIPES + blockIdx.x % DP_STRIPES, (unsigned long long)tot);
 }
@@ -1445,15 +1476,24 @@ __global__ void __launch_bounds__(64 * ASM_WAVES) dp_assemble_kernel(DpArgs A) {
     __shared__ unsigned long long lfp_sh[FP_LDS];
     __shared__ int32_t scratch_sh[ASM_WAVES][ASM_SCRATCH];
     DpState *S = A.st;
-    if (S->done) return;
-    if (S->skip == 1) return;   // (2: an inline step left this kernel its assembly)
-    unsigned long long *lfp = lfp_sh;   // used when A.V <= FP_LDS (an LDS pointer: ds_* atomics)
-    firstpos_begin(A, lfp);
-    const int cur = S->cur;
-    const ClauseList L = A.g[cur], O = A.g[cur ^ 1];
+    const int done = S->done, skip = S->skip, cur = S->cur;
     const int64_t ncl2 = S->ncl2, nr = S->nr, nn = S->nn, base = S->arena_base;
     const int64_t capA = S->capA, capB = S->capB, capR = S->capR;
     const int32_t var = S->var;
+    DP_KEEP(cur);
+    DP_KEEP(ncl2);
+    DP_KEEP(nr);
+    DP_KEEP(nn);
+    DP_KEEP(base);
+    DP_KEEP(capA);
+    DP_KEEP(capB);
+    DP_KEEP(capR);
+    DP_KEEP(var);
+    if (done) return;
+    if (skip == 1) return;   // (2: an inline step left this kernel its assembly)
+    unsigned long long *lfp = lfp_sh;   // used when A.V <= FP_LDS (an LDS pointer: ds_* atomics)
+    firstpos_begin(A, lfp);
+    const ClauseList L = A.g[cur], O = A.g[cur ^ 1];
     const int K = A.K, lane = lane_id(), wid = threadIdx.x >> 6;
     const int64_t tab = 2 * (capA + capB + capR);   // the three tables' slots
     const bool lds_ok = tab <= ASM_SCRATCH;
