@@ -943,6 +943,9 @@ def legs_main(args):
         r = run_one(a, 1, 0, 0)
         r["leg_wall_s"] = time.perf_counter() - t
         out[name] = r
+        # progress on stderr (inherited by the parent: a long default run keeps
+        # telling a watchdog it is alive; stdout carries only the result)
+        print(f"bench: leg {name!r} done in {r['leg_wall_s']:.1f} s", file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 
 
@@ -1022,6 +1025,8 @@ def main():
         print("bench: note: GPU_MAX_HW_QUEUES < streams + 1, the streams share hardware queues", file=sys.stderr)
     t_start = time.perf_counter()
     out = run_one(args, world, rank, local)
+    if rank == 0:
+        print(f"bench: {args.workload} done in {time.perf_counter() - t_start:.1f} s", file=sys.stderr, flush=True)
     legs = (world == 1 and not args.no_legs and not args.profile_steps and args.workload == "3sat-n100"
             and args.total == WORKLOADS["3sat-n100"][0] and not args.emulate_world)
     if legs and rank == 0:
@@ -1032,9 +1037,9 @@ def main():
                                 "--leg-cpu-seconds", str(args.leg_cpu_seconds)]
                                + (["--legs-hwq17"] if hwq else [])
                                + (["--no-cpu-baseline"] if args.no_cpu_baseline else []),
-                               capture_output=True, text=True, env=env)
+                               stdout=subprocess.PIPE, text=True, env=env)   # (stderr: the legs' progress)
             if r.returncode != 0:
-                raise SystemExit(f"bench: secondary configs failed:\n{r.stderr[-4000:]}")
+                raise SystemExit(f"bench: secondary configs failed (exit {r.returncode}; their stderr above)")
             got.update(json.loads(r.stdout.strip().splitlines()[-1]))
         # (DESIGN.md "Measurement": how the legs run and which answers configs[1])
         out["configs"] = {name: got[name] for name, _, _ in LEGS if name in got}
