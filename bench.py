@@ -615,7 +615,7 @@ def dp_roofline(stats, solves_per_s, floor_us):
     return {"bound": "launch-latency", "achieved": ach, "peak": peak, "unit": "launches/s", "frac": ach / peak,
             "peak_source": "measured: an empty chain of as many dependent one-block launches replayed from a HIP "
                            "graph (satmi_launch_chain_floor)", "floor_us_per_launch": floor_us,
-            "traffic": None, "kernel": "dp step chain (9 kernels per elimination step)",
+            "traffic": None, "kernel": "dp step chain (8 kernels per elimination step)",
             "launches_per_solve": launches, "device_ms_per_solve": dms,
             "us_per_launch": dms * 1e3 / launches if launches else None,
             "subset_tests_per_solve": sum(s["subset_tests"] for s in stats) / len(stats),

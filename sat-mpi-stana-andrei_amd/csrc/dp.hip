@@ -19,7 +19,9 @@
 //   pairs      resolvent key of every (pos, neg) pair, tautology / empty
 //              flags, the non-tautological pairs as a bitmap;
 //   hash       one representative per distinct resolvent: the FIRST pair (in
-//              pair order) holding that key, by atomicMin in a hash table;
+//              pair order) holding that key, by atomicMin in a hash table; each
+//              key's table slot into a stripe region (read in stripe order
+//              as the representatives' list by the next two kernels);
 //   remtest    every representative against the remaining clauses (2-D grid:
 //              representative tiles x rem chunks, rem keys broadcast from LDS);
 //   survlist   the representatives no rem clause subsumes (and the table
@@ -84,10 +86,7 @@ constexpr int DP_STRIPES = 64;
 #ifndef DP_GRID_ASM
 #define DP_GRID_ASM 2048
 #endif
-#ifndef DP_GRID_GATHER
-#define DP_GRID_GATHER 64
-#endif
-constexpr int DP_LAUNCHES_PER_STEP = 9;   // pop_split, pairs, hash, gather, remtest, survlist, survtest, kept, assemble
+constexpr int DP_LAUNCHES_PER_STEP = 8;   // pop_split, pairs, hash, remtest, survlist, survtest, kept, assemble
 
 // The solve's state, on the device.  Host writes it once per solve (and on a
 // resume); kernels read sizes from it and one thread of the single-workgroup
@@ -135,7 +134,7 @@ struct DpArgs {
     uint32_t *uslot;                // table slot of each distinct key
     int32_t *dropped, *hit;         // epoch stamps: representative subsumed by rem / survivor hit
     uint32_t *surv, *klist;         // survivors' pair indices; kept pairs in pair order
-    uint64_t *rkeys, *ukeys, *skeys;  // contiguous keys: rem clauses, representatives, survivors
+    uint64_t *rkeys, *skeys;          // contiguous keys: rem clauses, survivors
     // Per-step counters striped over DP_STRIPES words each (stripe = block
     // index mod DP_STRIPES): [0, S) representatives claimed per stripe, [S, 2S)
     // non-tautological pairs, [2S, 3S) subset tests.  One hot counter
@@ -1038,7 +1037,7 @@ __global__ void __launch_bounds__(256) dp_hash_kernel(DpArgs A) {
             }
         }
         const uint64_t bal = __ballot(claimed);
-        if (bal) {   // the slot into this block's stripe region (dp_gather_kernel packs the regions)
+        if (bal) {   // the slot into this block's stripe region (rep_slot reads the regions in order)
             const int st = blockIdx.x % DP_STRIPES;
             uint32_t base = 0;
             if (lane == 0) base = (uint32_t)atomicAdd(A.stripes + st, (unsigned long long)__popcll(bal));
@@ -1081,8 +1080,8 @@ __device__ __forceinline__ bool subset_of(const uint64_t *y, const KeyReg<KT> &x
 // l against the candidates of tile y with cand_ok(j) (all rem clauses; the
 // survivors earlier in pair order), marking stamp[x] = epoch at the first
 // subset; a lane whose x another block already marked stops.
-template <int KT, bool SURV>
-__device__ __forceinline__ void dp_test_items(const DpArgs &A, int64_t nx, int64_t ny, const uint64_t *xkeys,
+template <int KT, bool SURV, class XK>
+__device__ __forceinline__ void dp_test_items(const DpArgs &A, int64_t nx, int64_t ny, XK &&xkey,
                                               const uint64_t *ykeys, const uint32_t *ypair, int32_t *stamp,
                                               int32_t epoch, int &tests) {
     __shared__ __attribute__((aligned(16))) uint64_t tile[TEST_TILE * (KT ? KT : 1)];
@@ -1093,7 +1092,7 @@ __device__ __forceinline__ void dp_test_items(const DpArgs &A, int64_t nx, int64
         const int64_t tx = item % ntx, ty = item / ntx;
         const int64_t u = tx * TEST_TILE + tid;
         const bool valid = u < nx;
-        const uint64_t *xg = xkeys + (valid ? u : 0) * K;
+        const uint64_t *xg = xkey(valid ? u : 0);   // x's key words
         KeyReg<KT> x;
         if constexpr (KT > 0) {
 #pragma unroll
@@ -1180,35 +1179,12 @@ __device__ __forceinline__ void dp_test_items(const DpArgs &A, int64_t nx, int64
     }
 }
 
-// every representative against the remaining clauses (REF.py:124, remaining
-// part); the representatives' keys are gathered first (x side, contiguous)
-template <int KT>
-__global__ void __launch_bounds__(TEST_TILE) dp_remtest_kernel(DpArgs A) {
-    __shared__ int wsum[4];
-    DpState *S = A.st;
-    const int done = S->done, skip = S->skip;
-    const uint64_t fe = S->first_empty;
-    const int64_t nuniq = S->nuniq, nr = S->nr;
-    const int32_t epoch = S->epoch;
-    DP_KEEP(nuniq);
-    DP_KEEP(nr);
-    DP_KEEP(epoch);
-    if (done || skip || fe != DP_EMPTY) return;
-    int tests = 0;
-    dp_test_items<KT, false>(A, nuniq, nr, A.ukeys, A.rkeys, nullptr, A.dropped, epoch, tests);
-    const int tot = block_sum(tests, wsum);
-    if (threadIdx.x == 0 && tot) atomicAdd(A.stripes + 2 * DP_STRIPES + blockIdx.x % DP_STRIPES, (unsigned long long)tot);
-}
-
-// the distinct representatives, packed from the stripe regions: their table
-// slots (uslot) and keys (ukeys, remtest's x side), contiguous; nuniq.  Grid:
-// x blocks per stripe, DP_STRIPES in y.
-__global__ void __launch_bounds__(256) dp_gather_kernel(DpArgs A) {
-    __shared__ int64_t pre[DP_STRIPES + 1];
-    DpState *S = A.st;
-    const int done = S->done, skip = S->skip;
-    const uint64_t fe = S->first_empty;
-    if (done || skip || fe != DP_EMPTY) return;
+// The distinct representatives are the hash kernel's claims, in stripe
+// regions (ustage: stripe st holds stripes[st] table slots).  Representative u
+// is slot t = u - pre[st] of the stripe st with pre[st] <= u < pre[st + 1];
+// remtest and survlist read them there (no packing launch between them).
+// pre: DP_STRIPES + 1 prefix sums in LDS, filled by every thread calling this.
+__device__ __forceinline__ int64_t rep_prefix(const DpArgs &A, int64_t *pre) {
     if (threadIdx.x == 0) {
         int64_t acc = 0;
         for (int t = 0; t < DP_STRIPES; ++t) {
@@ -1216,30 +1192,55 @@ __global__ void __launch_bounds__(256) dp_gather_kernel(DpArgs A) {
             acc += (int64_t)A.stripes[t];
         }
         pre[DP_STRIPES] = acc;
-        if (blockIdx.x == 0 && blockIdx.y == 0) S->nuniq = acc;
     }
     __syncthreads();
-    const int st = blockIdx.y, K = A.K;
-    const int64_t n = pre[st + 1] - pre[st], u0 = pre[st];
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t slot = A.ustage[(uint64_t)st * A.pair_cap + t];
-        A.uslot[u0 + t] = slot;
-        const uint64_t p = A.table[slot];
-        for (int w = 0; w < K; ++w) A.ukeys[(u0 + t) * K + w] = A.rbits[p * K + w];
-    }
+    return pre[DP_STRIPES];
+}
+// the table slot of representative u (u < pre[DP_STRIPES])
+__device__ __forceinline__ uint32_t rep_slot(const DpArgs &A, const int64_t *pre, int64_t u) {
+    int lo = 0;   // the last stripe whose region starts at or before u
+#pragma unroll
+    for (int half = DP_STRIPES / 2; half >= 1; half >>= 1)
+        lo = pre[lo + half] <= u ? lo + half : lo;
+    return A.ustage[(uint64_t)lo * A.pair_cap + (uint64_t)(u - pre[lo])];
+}
+
+// every representative against the remaining clauses (REF.py:124, remaining
+// part); a representative's key is read through its table slot (x side)
+template <int KT>
+__global__ void __launch_bounds__(TEST_TILE) dp_remtest_kernel(DpArgs A) {
+    __shared__ int wsum[4];
+    __shared__ int64_t pre[DP_STRIPES + 1];
+    DpState *S = A.st;
+    const int done = S->done, skip = S->skip;
+    const uint64_t fe = S->first_empty;
+    const int64_t nr = S->nr;
+    const int32_t epoch = S->epoch;
+    DP_KEEP(nr);
+    DP_KEEP(epoch);
+    if (done || skip || fe != DP_EMPTY) return;
+    const int64_t nuniq = rep_prefix(A, pre);
+    if (blockIdx.x == 0 && threadIdx.x == 0) S->nuniq = nuniq;
+    const int K = A.K;
+    int tests = 0;
+    dp_test_items<KT, false>(
+        A, nuniq, nr, [&](int64_t u) { return A.rbits + A.table[rep_slot(A, pre, u)] * (uint64_t)K; }, A.rkeys,
+        nullptr, A.dropped, epoch, tests);
+    const int tot = block_sum(tests, wsum);
+    if (threadIdx.x == 0 && tot) atomicAdd(A.stripes + 2 * DP_STRIPES + blockIdx.x % DP_STRIPES, (unsigned long long)tot);
 }
 
 // the representatives no rem clause subsumes (pair index + key, contiguous);
 // every used table slot cleared for the next step
 __global__ void __launch_bounds__(256) dp_survlist_kernel(DpArgs A) {
+    __shared__ int64_t pre[DP_STRIPES + 1];
     DpState *S = A.st;
     const int done = S->done, skip = S->skip;
     const uint64_t fe = S->first_empty;
-    const int64_t nuniq = S->nuniq;
     const int32_t epoch = S->epoch;
-    DP_KEEP(nuniq);
     DP_KEEP(epoch);
     if (done || skip || fe != DP_EMPTY) return;
+    const int64_t nuniq = rep_prefix(A, pre);
     const int lane = lane_id(), K = A.K, tid = threadIdx.x;
     __shared__ int wcnt[4];
     __shared__ uint32_t bbase;
@@ -1250,7 +1251,7 @@ __global__ void __launch_bounds__(256) dp_survlist_kernel(DpArgs A) {
         bool keep = false;
         uint32_t p = 0;
         if (u < nuniq) {
-            const uint32_t s = A.uslot[u];
+            const uint32_t s = rep_slot(A, pre, u);
             p = (uint32_t)A.table[s];
             A.table[s] = DP_EMPTY;
             keep = A.dropped[u] != epoch;
@@ -1265,7 +1266,7 @@ __global__ void __launch_bounds__(256) dp_survlist_kernel(DpArgs A) {
             uint32_t at = bbase + __popcll(bal & lanemask_lt());
             for (int w = 0; w < (tid >> 6); ++w) at += wcnt[w];
             A.surv[at] = p;
-            for (int w = 0; w < K; ++w) A.skeys[(uint64_t)at * K + w] = A.ukeys[u * K + w];
+            for (int w = 0; w < K; ++w) A.skeys[(uint64_t)at * K + w] = A.rbits[(uint64_t)p * K + w];
         }
         __syncthreads();
     }
@@ -1285,7 +1286,9 @@ __global__ void __launch_bounds__(TEST_TILE) dp_survtest_kernel(DpArgs A) {
     DP_KEEP(epoch);
     if (done || skip || fe != DP_EMPTY) return;
     int tests = 0;
-    dp_test_items<KT, true>(A, nsurv, nsurv, A.skeys, A.skeys, A.surv, A.hit, epoch, tests);
+    const int K = A.K;
+    dp_test_items<KT, true>(
+        A, nsurv, nsurv, [&](int64_t u) { return A.skeys + u * K; }, A.skeys, A.surv, A.hit, epoch, tests);
     const int tot = block_sum(tests, wsum);
     if (threadIdx.x == 0 && tot) atomicAdd(A.stripes + 2 * DP_STRIPES + blockIdx.x % DP_STRIPES, (unsigned long long)tot);
 }
@@ -1673,7 +1676,7 @@ struct DpGraph {
 struct DpWork {
     Buf d_off, d_lits, d_v2d, d_d2v, state, firstpos, order, popscratch, trace;
     Buf plist, nlist, rlist, rbits, ntbits, table, uslot, dropped, hit, surv, klist, keptbits, xs, arena;
-    Buf rkeys, ukeys, skeys, ustage, stripes;
+    Buf rkeys, skeys, ustage, stripes;
     Gen g[2];
     int64_t ncl_cap = 0, pair_cap = 0, arena_cap = 0, xs_cap = 0;
     uint64_t tslots = 0;
@@ -1759,7 +1762,6 @@ int grow_pairs(DpWork &W, int64_t npairs, int K) {
     DP_TRY(W.uslot.need(4 * (size_t)cap, s));
     DP_TRY(W.surv.need(4 * (size_t)cap, s));
     DP_TRY(W.klist.need(4 * (size_t)cap, s));
-    DP_TRY(W.ukeys.need(8 * (size_t)cap * K, s));
     DP_TRY(W.ustage.need(4 * (size_t)DP_STRIPES * cap, s));
     DP_TRY(W.skeys.need(8 * (size_t)cap * K, s));
     DP_TRY(W.dropped.need(4 * (size_t)cap, s, 0, 0));
@@ -1776,7 +1778,6 @@ int grow_pairs(DpWork &W, int64_t npairs, int K) {
     W.tslots = pw;
     W.pair_cap = std::min<int64_t>((int64_t)(W.rbits.cap / (8 * (size_t)K)), (int64_t)(W.tslots / 2));
     W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.uslot.cap / 4));
-    W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.ukeys.cap / (8 * (size_t)K)));
     W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.ustage.cap / (4 * (size_t)DP_STRIPES)));
     W.pair_cap = std::min<int64_t>(W.pair_cap, (int64_t)(W.skeys.cap / (8 * (size_t)K)));
     W.pair_cap = std::min<int64_t>(W.pair_cap, (1ll << 31) - 1);
@@ -1939,7 +1940,6 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         a.surv = Wk.surv.as<uint32_t>();
         a.klist = Wk.klist.as<uint32_t>();
         a.rkeys = Wk.rkeys.as<uint64_t>();
-        a.ukeys = Wk.ukeys.as<uint64_t>();
         a.skeys = Wk.skeys.as<uint64_t>();
         a.stripes = Wk.stripes.as<unsigned long long>();
         a.ustage = Wk.ustage.as<uint32_t>();
@@ -1981,8 +1981,6 @@ extern "C" int satmi_dp_host(int nclauses, const int32_t *h_clause_off, const in
         else hipLaunchKernelGGL(dp_pop_split_kernel<false>, dim3(1), dim3(POP_THREADS), 0, s, a);
         hipLaunchKernelGGL(dp_pairs_kernel, dim3(gp), dim3(256), 0, s, a);
         hipLaunchKernelGGL(dp_hash_kernel, dim3(gp), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(dp_gather_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(DP_GRID_GATHER, a.pair_cap / (DP_STRIPES * 256))), DP_STRIPES),
-                           dim3(256), 0, s, a);
         const dim3 gt((unsigned)std::min<int64_t>(DP_GRID_TEST, std::max<int64_t>(64, a.pair_cap / 256)));
         switch (a.K) {
             case 2: hipLaunchKernelGGL(dp_remtest_kernel<2>, gt, dim3(TEST_TILE), 0, s, a); break;
